@@ -1,0 +1,227 @@
+#!/usr/bin/env python3
+"""Throughput bench of the batched MultiAgentGraphConstrainEnv step path.
+
+Metric (BASELINE.json): agent-steps/sec, cooperative navigation, 24 agents x
+8192 envs per MI355X (the headline config; N GPUs = weak scaling, each rank
+owns 8192 envs with global Philox env ids, BASELINE configs[4] at N=8).
+
+A "step" = one env.step of every env on the GPU: action force, pairwise
+contact physics, integration, reward, collision cost, done/auto-reset, node
+features and the packed COO edge list (two kernels). Actions
+are pre-generated on device (100 x B x N int32, uniform over the 5 discrete
+actions) so the timed region has no host work; the K timed steps are
+replayed from HIP graphs of one episode (100 steps) each, with the per-episode
+RCCL all-reduce of episode metrics between chunks when N > 1.
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
+       torchrun --nproc-per-node N bench.py --gpus N ...
+Prints ONE JSON line on rank 0 (diagnostics go to stderr).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT / "gs-marl_amd"))
+sys.path.insert(0, str(ROOT))
+
+METRIC = "agent-steps/sec, coop-navigation 24 agents × 8192 envs, at 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0   # MI355X HBM3E spec peak (MI355X_MICROARCH.md: 8.0 TB/s; 6.29 measured copy)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def step_kernel_bytes(B, N, No, EL, action_bytes):
+    """Algorithmic HBM bytes of one gsm_step_kernel launch."""
+    E = 2 * N + No
+    reads = 8 * E + 8 * N + action_bytes * N + 16
+    writes = 8 * N + 8 * N + 28 * E + 4 * N + 4 * N + 1 + 4 + 16 + 1
+    reset = ((E - N) * 8 + 8) / EL          # amortised re-layout write
+    return B * (reads + writes + reset)
+
+
+def emit_kernel_bytes(B, N, No, total_edges):
+    """Algorithmic HBM bytes of one gsm_emit_edges_kernel launch."""
+    E = 2 * N + No
+    return B * (8 * E + 4 + 8) + 12 * total_edges
+
+
+def cpu_baseline(n_agents, seconds):
+    """Reference-structure CPU restatement (object-per-entity MPE, fp64,
+    Python pair loop: oracle/mpe_ref.py) on one host core."""
+    import numpy as np
+    from oracle import mpe_ref
+    from oracle.batch_ref import make_cfg
+    env = mpe_ref.GraphConstrainEnv(make_cfg(n_agents=n_agents))
+    env.reset(seed=0)
+    rng = np.random.default_rng(0)
+    eye = np.eye(5)
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        env.step(list(eye[rng.integers(0, 5, size=n_agents)]))
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return dict(value=steps * n_agents / el, unit="agent-steps/s", cores=1, kind="port",
+                sample=f"1 env x {steps} steps ({el:.1f} s) of oracle/mpe_ref.py GraphConstrainEnv.step "
+                       f"(object-per-entity MPE restatement, fp64, Python pair loop), N={n_agents}, "
+                       f"1 host core; the reference's own CPU path is absent (readme.md:1)")
+
+
+def pmc_traffic(key):
+    """HBM bytes per step-kernel launch from the committed rocprofv3 PMC
+    summary (profiles/pmc_traffic.json, written by tools/pmc_traffic.py)."""
+    p = ROOT / "profiles" / "pmc_traffic.json"
+    if not p.exists():
+        return None
+    try:
+        d = json.loads(p.read_text())
+        return d.get(key, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=300)
+    ap.add_argument("--warmup", type=int, default=50)
+    ap.add_argument("--n-agents", type=int, default=24)
+    ap.add_argument("--n-envs", type=int, default=8192, help="envs per GPU")
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing-events", action="store_true",
+                    help="capture without per-kernel HIP event nodes (roofline then null)")
+    ap.add_argument("--eager", action="store_true", help="launch steps eagerly instead of HIP graphs")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+
+    from gsmarl_amd import EnvConfig, GpuBatchEnv
+    from gsmarl_amd.distributed import all_reduce_metrics, max_over_ranks, shard_config
+
+    N, B = args.n_agents, args.n_envs
+    cfg = shard_config(EnvConfig(n_agents=N, n_envs=B, seed=1234), rank, world)
+    env = GpuBatchEnv(cfg, dev)
+    EL = cfg.episode_length
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1000 + rank)
+    actions = torch.randint(0, 5, (EL, B, N), dtype=torch.int32, device=dev, generator=gen)
+    env.reset(seed=cfg.seed, sync_edges=False)
+
+    K, W = args.steps, args.warmup
+    chunk = min(K, EL)
+    n_chunks, rem = divmod(K, chunk)
+    timing = not args.no_timing_events and not args.eager
+    if not args.eager:
+        if W > 0:
+            env.capture(actions, W, timing=False, slot=2)
+        env.capture(actions, chunk, timing=timing, slot=0)
+        if rem:
+            env.capture(actions, rem, timing=False, slot=1)
+    # warmup
+    if W > 0:
+        if args.eager:
+            for t in range(W):
+                env.step(actions[t % EL], sync_edges=False)
+        else:
+            env.replay(2)
+    torch.cuda.synchronize()
+    metrics = torch.zeros(3, dtype=torch.float64, device=dev)
+
+    def run_chunk(n, slot):
+        if args.eager:
+            for t in range(n):
+                env.step(actions[t % EL], sync_edges=False)
+        else:
+            env.replay(slot)
+
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n_chunks):
+        run_chunk(chunk, 0)
+        if world > 1:   # the only collective: per-episode metrics (RCCL/xGMI)
+            metrics.copy_(env.episode_metrics())
+            all_reduce_metrics(metrics)
+    if rem:
+        run_chunk(rem, 1)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    elapsed = max_over_ranks(elapsed, device=dev) if world > 1 else elapsed
+
+    total_edges = int(env.t["edge_ptr"][B].item())
+    value = world * B * N * K / elapsed
+    ms_per_step = elapsed / K * 1e3
+
+    roofline = None
+    kern = None
+    if timing:
+        step_ms, emit_ms = env.graph_kernel_ms(0)
+        sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4)
+        eb = emit_kernel_bytes(B, N, cfg.n_obstacles, total_edges)
+        kern = dict(step_kernel_ms=step_ms, emit_kernel_ms=emit_ms,
+                    step_kernel_bytes=sb, emit_kernel_bytes=eb,
+                    step_kernel_gbs=sb / (step_ms * 1e-3) / 1e9,
+                    emit_kernel_gbs=eb / (emit_ms * 1e-3) / 1e9)
+        dom = "step" if step_ms >= emit_ms else "emit"
+        ach = kern[f"{dom}_kernel_gbs"]
+        roofline = dict(kernel="gsm_step_kernel" if dom == "step" else "gsm_emit_edges_kernel",
+                        bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=round(ach / HBM_PEAK_GBS, 4),
+                        algorithmic_bytes_per_launch=int(kern[f"{dom}_kernel_bytes"]),
+                        mean_launch_ms=round(kern[f"{dom}_kernel_ms"], 5),
+                        traffic=pmc_traffic(f"{dom}:N{N}:B{B}"))
+        log(f"kernels: {json.dumps(kern)}")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(N, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC, "value": round(value, 1), "unit": "agent-steps/s", "n_gpus": world,
+            "steps": K, "warmup": W, "ms_per_step": round(ms_per_step, 5), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic: Philox4x32-10 layouts, uniform random discrete actions pre-generated on device",
+            "config": {"workload": f"cooperative_navigation {N} agents x {B} envs per GPU "
+                                   f"({N} goals, {cfg.n_obstacles} obstacles; BASELINE headline / configs[4] shard)",
+                       "n_agents": N, "n_envs_per_gpu": B, "global_envs": world * B,
+                       "episode_length": EL, "mean_edges_per_env": round(total_edges / B, 2),
+                       "parallelism": f"env-sharded x{world} (no data-path collective)",
+                       "launch": "eager" if args.eager else "hip-graph per 100-step episode"},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,354 @@
+// gsm_abi.hip — extern "C" boundary of libgsm.so (declared in include/gsm.h).
+//
+// Host-only bookkeeping: validate the config, derive the fp32 constants the
+// kernels use (same fp32 operations as oracle/batch_ref.py:Spec), borrow the
+// caller's device buffers, launch, and optionally capture whole multi-step
+// rollouts into a HIP graph. No allocation and no synchronisation happens in
+// gsm_step / gsm_reset / gsm_observe.
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "gsm.h"
+#include "gsm_internal.h"
+
+struct gsm_handle {
+    gsm_config cfg;
+    gsm_sizes sz;
+    gsm::DevParams dp;      // constants + bound buffers
+    bool bound = false;
+    std::string err;
+    // graph capture
+    hipStream_t cap_stream = nullptr;
+    struct Slot {
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+        std::vector<hipEvent_t> events;   // 3 per step when timing
+        int steps = 0;
+    } slots[GSM_GRAPH_SLOTS];
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(gsm_handle *h, int code, const std::string &msg) {
+    if (h) h->err = msg;
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(gsm_handle *h, hipError_t e, const char *where) {
+    char buf[256];
+    snprintf(buf, sizeof buf, "%s: hipError %d (%s)", where, (int)e, hipGetErrorString(e));
+    return fail(h, GSM_EHIP, buf);
+}
+
+int align16(int x) { return (x + 15) & ~15; }
+
+int check_config(const gsm_config *c, std::string *why) {
+    if (!c) { *why = "config is NULL"; return GSM_EINVAL; }
+    if (c->abi_version != GSM_ABI_VERSION) {
+        *why = "abi_version mismatch (library " + std::to_string(GSM_ABI_VERSION) + ", caller " +
+               std::to_string(c->abi_version) + ")";
+        return GSM_EINVAL;
+    }
+    if (c->scenario != GSM_SCEN_NAVIGATION) { *why = "unsupported scenario"; return GSM_EINVAL; }
+    if (c->n_envs < 1) { *why = "n_envs must be >= 1"; return GSM_EINVAL; }
+    if (c->n_agents < 1 || c->n_agents > 1024) { *why = "n_agents must be in [1, 1024]"; return GSM_EINVAL; }
+    if (c->n_obstacles < 0 || c->n_obstacles > 1024) { *why = "n_obstacles must be in [0, 1024]"; return GSM_EINVAL; }
+    if (c->episode_length < 1) { *why = "episode_length must be >= 1"; return GSM_EINVAL; }
+    if (!(c->dt > 0) || !(c->mass > 0) || !(c->contact_margin > 0) || !(c->world_half > 0)) {
+        *why = "dt, mass, contact_margin and world_half must be > 0";
+        return GSM_EINVAL;
+    }
+    if (!(c->damping >= 0 && c->damping <= 1)) { *why = "damping must be in [0, 1]"; return GSM_EINVAL; }
+    if (!(c->sense_radius >= 0) || !(c->contact_cutoff > 0)) {
+        *why = "sense_radius must be >= 0 and contact_cutoff > 0";
+        return GSM_EINVAL;
+    }
+    return GSM_OK;
+}
+
+void fill_sizes(const gsm_config *c, gsm_sizes *s) {
+    const int N = c->n_agents, No = c->n_obstacles, M = N + No;
+    s->n_entities = 2 * N + No;
+    s->node_feat_dim = 7;
+    s->obs_dim = 6;
+    s->envs_per_block = gsm::kWavesPerBlock;
+    s->n_blocks = (c->n_envs + gsm::kWavesPerBlock - 1) / gsm::kWavesPerBlock;
+    s->max_edges_per_env = M * (M - 1) + 2 * N;
+    s->edge_capacity = (int64_t)c->n_envs * s->max_edges_per_env;
+}
+
+// fp32 constants, formed exactly like oracle/batch_ref.py:Spec (fp32 mode).
+void derive(const gsm_config *c, gsm::DevParams *p) {
+    memset(p, 0, sizeof *p);
+    const int N = c->n_agents, No = c->n_obstacles;
+    p->B = c->n_envs;
+    p->N = N;
+    p->No = No;
+    p->E = 2 * N + No;
+    p->M = N + No;
+    // slices per agent so that N*S lanes of the wave share the contact loop
+    int S = N <= gsm::kWave ? gsm::kWave / N : 1;
+    if (S > p->M) S = p->M;
+    if (S < 1) S = 1;
+    p->S = S;
+    p->EL = c->episode_length;
+    p->auto_reset = c->auto_reset != 0;
+    p->shared_reward = c->shared_reward != 0;
+    p->seed_lo = (uint32_t)(c->seed & 0xFFFFFFFFull);
+    p->seed_hi = (uint32_t)(c->seed >> 32);
+    p->env_base = c->env_base;
+    p->wave_lds_step = align16(8 * p->E + 8 * N + 12 * S * N);
+    p->wave_lds_emit = align16(8 * p->E);
+    const float L = c->world_half;
+    p->L = L;
+    p->twoL = L * 2.0f;
+    p->dt = c->dt;
+    p->omd = 1.0f - c->damping;
+    p->mass = c->mass;
+    p->cf = c->contact_force;
+    p->k = c->contact_margin;
+    p->inv_k = 1.0f / c->contact_margin;
+    p->sens = c->sensitivity;
+    p->max_speed = c->max_speed;
+    const float R = c->sense_radius;
+    p->R2 = R * R;
+    const float sa = c->agent_size, so = c->obstacle_size;
+    p->dmin_aa = sa + sa;
+    p->dmin_ao = sa + so;
+    p->dmin2_aa = p->dmin_aa * p->dmin_aa;
+    p->dmin2_ao = p->dmin_ao * p->dmin_ao;
+    // beyond d - dmin > cutoff*k the pair force is below cf*k*exp(-cutoff)
+    // (4e-19 at the default cutoff 40): skipped (contact cutoff)
+    const float caa = p->dmin_aa + c->contact_cutoff * c->contact_margin;
+    const float cao = p->dmin_ao + c->contact_cutoff * c->contact_margin;
+    p->cut2_aa = caa * caa;
+    p->cut2_ao = cao * cao;
+}
+
+hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
+
+int launch(gsm_handle *h, int mode, const void *actions, int fmt, const uint8_t *mask, int reseed,
+           hipStream_t s) {
+    if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
+    if (!h->bound) return fail(h, GSM_ESTATE, "gsm_bind has not been called");
+    if (mode == GSM_MODE_STEP) {
+        if (!actions) return fail(h, GSM_EINVAL, "actions is NULL");
+        if (fmt < GSM_ACT_ONEHOT || fmt > GSM_ACT_CONT) return fail(h, GSM_EINVAL, "bad action_fmt");
+    }
+    gsm::DevParams p = h->dp;
+    p.mode = mode;
+    p.actions = actions;
+    p.action_fmt = fmt;
+    p.env_mask = mask;
+    p.reseed = reseed;
+    const hipError_t e = gsm::launch_step(p, s);
+    if (e != hipSuccess) return hip_fail(h, e, "kernel launch");
+    return GSM_OK;
+}
+
+void drop_slot(gsm_handle::Slot &s) {
+    if (s.exec) (void)hipGraphExecDestroy(s.exec);
+    if (s.graph) (void)hipGraphDestroy(s.graph);
+    for (hipEvent_t ev : s.events) (void)hipEventDestroy(ev);
+    s.exec = nullptr;
+    s.graph = nullptr;
+    s.events.clear();
+    s.steps = 0;
+}
+
+void drop_graph(gsm_handle *h) {
+    for (auto &s : h->slots) drop_slot(s);
+}
+
+bool bad_slot(int32_t slot) { return slot < 0 || slot >= GSM_GRAPH_SLOTS; }
+
+}  // namespace
+
+extern "C" {
+
+int gsm_abi_version(void) { return GSM_ABI_VERSION; }
+
+int gsm_query_sizes(const gsm_config *cfg, gsm_sizes *out) {
+    std::string why;
+    const int rc = check_config(cfg, &why);
+    if (rc) return fail(nullptr, rc, why);
+    if (!out) return fail(nullptr, GSM_EINVAL, "sizes is NULL");
+    fill_sizes(cfg, out);
+    if (out->edge_capacity >= (int64_t)1 << 31 ||
+        (int64_t)cfg->n_envs * out->n_entities >= (int64_t)1 << 31)
+        return fail(nullptr, GSM_EINVAL, "n_envs too large for int32 edge ids/offsets; shard the envs");
+    return GSM_OK;
+}
+
+int gsm_create(const gsm_config *cfg, gsm_handle **out) {
+    if (!out) return fail(nullptr, GSM_EINVAL, "out is NULL");
+    *out = nullptr;
+    gsm_sizes sz;
+    const int rc = gsm_query_sizes(cfg, &sz);
+    if (rc) return rc;
+    gsm_handle *h = new (std::nothrow) gsm_handle();
+    if (!h) return fail(nullptr, GSM_EINVAL, "out of host memory");
+    h->cfg = *cfg;
+    h->sz = sz;
+    derive(cfg, &h->dp);
+    h->dp.edge_capacity = sz.edge_capacity;
+    *out = h;
+    return GSM_OK;
+}
+
+int gsm_bind(gsm_handle *h, const gsm_buffers *b) {
+    if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
+    if (!b) return fail(h, GSM_EINVAL, "buffers is NULL");
+    const void *req[] = {b->pos, b->vel, b->step_count, b->episode, b->ep_acc, b->ep_last,
+                         b->node_feat, b->reward, b->cost, b->done, b->edge_count,
+                         b->block_edge_sum, b->edge_ptr, b->edge_index, b->edge_attr};
+    for (const void *q : req)
+        if (!q) return fail(h, GSM_EINVAL, "a required buffer pointer is NULL");
+    if (((uintptr_t)b->pos | (uintptr_t)b->vel | (uintptr_t)b->ep_acc | (uintptr_t)b->ep_last) & 7)
+        return fail(h, GSM_EINVAL, "pos/vel/ep_acc/ep_last must be 8-byte aligned");
+    gsm::DevParams &p = h->dp;
+    p.pos = (float2 *)b->pos;
+    p.vel = (float2 *)b->vel;
+    p.step_count = b->step_count;
+    p.episode = b->episode;
+    p.ep_acc = (float2 *)b->ep_acc;
+    p.ep_last = (float2 *)b->ep_last;
+    p.node_feat = b->node_feat;
+    p.reward = b->reward;
+    p.cost = b->cost;
+    p.done = b->done;
+    p.edge_count = b->edge_count;
+    p.block_edge_sum = b->block_edge_sum;
+    p.edge_ptr = b->edge_ptr;
+    p.edge_index = b->edge_index;
+    p.edge_attr = b->edge_attr;
+    h->bound = true;
+    drop_graph(h);   // a captured graph holds the old pointers
+    return GSM_OK;
+}
+
+int gsm_reset(gsm_handle *h, uint64_t seed, int reseed, const uint8_t *env_mask, void *stream) {
+    if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
+    if (reseed && seed != h->cfg.seed) {
+        h->cfg.seed = seed;
+        h->dp.seed_lo = (uint32_t)(seed & 0xFFFFFFFFull);
+        h->dp.seed_hi = (uint32_t)(seed >> 32);
+        drop_graph(h);   // captured auto-resets would use the old key
+    }
+    return launch(h, GSM_MODE_RESET, nullptr, 0, env_mask, reseed ? 1 : 0, as_stream(stream));
+}
+
+int gsm_step(gsm_handle *h, const void *actions, int action_fmt, void *stream) {
+    return launch(h, GSM_MODE_STEP, actions, action_fmt, nullptr, 0, as_stream(stream));
+}
+
+int gsm_observe(gsm_handle *h, void *stream) {
+    return launch(h, GSM_MODE_OBSERVE, nullptr, 0, nullptr, 0, as_stream(stream));
+}
+
+int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t stride,
+                      int32_t n_actions, int32_t n_steps, int action_fmt, int with_timing) {
+    if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
+    if (!h->bound) return fail(h, GSM_ESTATE, "gsm_bind has not been called");
+    if (bad_slot(slot)) return fail(h, GSM_EINVAL, "bad graph slot");
+    if (!actions || n_actions < 1 || n_steps < 1 || stride < 0)
+        return fail(h, GSM_EINVAL, "bad capture arguments");
+    if (action_fmt < GSM_ACT_ONEHOT || action_fmt > GSM_ACT_CONT) return fail(h, GSM_EINVAL, "bad action_fmt");
+    gsm_handle::Slot &sl = h->slots[slot];
+    drop_slot(sl);
+    hipError_t e;
+    if (!h->cap_stream) {
+        e = hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking);
+        if (e != hipSuccess) return hip_fail(h, e, "hipStreamCreate");
+    }
+    if (with_timing) {
+        sl.events.resize(3 * (size_t)n_steps, nullptr);
+        for (auto &ev : sl.events) {
+            e = hipEventCreate(&ev);
+            if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipEventCreate"); }
+        }
+    }
+    e = hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal);
+    if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipStreamBeginCapture"); }
+    gsm::DevParams p = h->dp;
+    p.mode = GSM_MODE_STEP;
+    p.action_fmt = action_fmt;
+    p.env_mask = nullptr;
+    p.reseed = 0;
+    hipError_t first = hipSuccess;
+    for (int t = 0; t < n_steps && first == hipSuccess; ++t) {
+        p.actions = (const char *)actions + (int64_t)(t % n_actions) * stride;
+        if (with_timing) first = hipEventRecord(sl.events[3 * t], h->cap_stream);
+        if (first == hipSuccess) first = gsm::launch_step_kernel(p, h->cap_stream);
+        if (with_timing && first == hipSuccess) first = hipEventRecord(sl.events[3 * t + 1], h->cap_stream);
+        if (first == hipSuccess) first = gsm::launch_emit_kernel(p, h->cap_stream);
+        if (with_timing && first == hipSuccess) first = hipEventRecord(sl.events[3 * t + 2], h->cap_stream);
+    }
+    hipGraph_t g = nullptr;
+    e = hipStreamEndCapture(h->cap_stream, &g);
+    if (first != hipSuccess) { if (g) (void)hipGraphDestroy(g); drop_slot(sl); return hip_fail(h, first, "capture"); }
+    if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipStreamEndCapture"); }
+    sl.graph = g;
+    e = hipGraphInstantiate(&sl.exec, g, nullptr, nullptr, 0);
+    if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipGraphInstantiate"); }
+    e = hipGraphUpload(sl.exec, h->cap_stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->cap_stream);
+    if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipGraphUpload"); }
+    sl.steps = n_steps;
+    return GSM_OK;
+}
+
+int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream) {
+    if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
+    if (bad_slot(slot)) return fail(h, GSM_EINVAL, "bad graph slot");
+    if (!h->slots[slot].exec) return fail(h, GSM_ESTATE, "no graph captured in this slot");
+    const hipError_t e = hipGraphLaunch(h->slots[slot].exec, as_stream(stream));
+    if (e != hipSuccess) return hip_fail(h, e, "hipGraphLaunch");
+    return GSM_OK;
+}
+
+int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_ms, float *emit_ms) {
+    if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
+    if (bad_slot(slot)) return fail(h, GSM_EINVAL, "bad graph slot");
+    const gsm_handle::Slot &sl = h->slots[slot];
+    if (!sl.exec || sl.events.empty()) return fail(h, GSM_ESTATE, "no timed graph in this slot");
+    double a = 0, b = 0;
+    for (int t = 0; t < sl.steps; ++t) {
+        float x = 0, y = 0;
+        hipError_t e = hipEventElapsedTime(&x, sl.events[3 * t], sl.events[3 * t + 1]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&y, sl.events[3 * t + 1], sl.events[3 * t + 2]);
+        if (e != hipSuccess) return hip_fail(h, e, "hipEventElapsedTime");
+        a += x;
+        b += y;
+    }
+    if (step_ms) *step_ms = (float)(a / sl.steps);
+    if (emit_ms) *emit_ms = (float)(b / sl.steps);
+    return GSM_OK;
+}
+
+int gsm_destroy(gsm_handle *h) {
+    if (!h) return GSM_OK;
+    drop_graph(h);
+    if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
+    delete h;
+    return GSM_OK;
+}
+
+int gsm_last_error(const gsm_handle *h, char *buf, size_t len) {
+    const std::string &m = h ? h->err : g_err;
+    if (buf && len) {
+        const size_t n = m.size() < len - 1 ? m.size() : len - 1;
+        memcpy(buf, m.data(), n);
+        buf[n] = 0;
+    }
+    return (int)m.size();
+}
+
+}  // extern "C"

@@ -1,0 +1,44 @@
+// Internal (non-ABI) declarations shared by gsm_kernels.hip and gsm_abi.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gsm {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;              // one env per wave
+constexpr int kBlock = kWave * kWavesPerBlock;
+
+// Everything a launch needs, passed by value (kernarg segment, < 4 KB).
+// fp32 constants are formed on the host exactly as oracle/batch_ref.py:Spec
+// forms them in fp32 mode (gsm_abi.hip: derive()).
+struct DevParams {
+    int32_t B, N, No, E, M, S, EL, auto_reset, shared_reward;
+    int32_t mode, action_fmt, reseed;
+    uint32_t seed_lo, seed_hi;
+    int64_t env_base;
+    int32_t wave_lds_step, wave_lds_emit;      // bytes of LDS per wave
+    float dt, omd, mass, cf, k, inv_k, sens, max_speed, L, twoL, R2;
+    float dmin_aa, dmin_ao, dmin2_aa, dmin2_ao, cut2_aa, cut2_ao;
+    // caller-owned device buffers (see gsm.h gsm_buffers)
+    float2 *pos, *vel;
+    int32_t *step_count, *episode;
+    float2 *ep_acc, *ep_last;
+    float *node_feat, *reward, *cost;
+    uint8_t *done;
+    int32_t *edge_count, *block_edge_sum;
+    int64_t *edge_ptr;
+    int32_t *edge_index;
+    float *edge_attr;
+    int64_t edge_capacity;
+    const void *actions;
+    const uint8_t *env_mask;
+};
+
+// Launch the step kernel (physics / reset / observe by p.mode) and the edge
+// emitter for all B envs on `s`. Returns the first hipError_t.
+hipError_t launch_step(const DevParams &p, hipStream_t s);
+hipError_t launch_step_kernel(const DevParams &p, hipStream_t s);
+hipError_t launch_emit_kernel(const DevParams &p, hipStream_t s);
+
+}  // namespace gsm

@@ -1,0 +1,11 @@
+"""gsmarl_amd — MI355X-native batched step path of GS-MARL's
+MultiAgentGraphConstrainEnv (HIP kernels in libgsm.so behind a C ABI)."""
+from .config import EnvConfig
+from .batch import GpuBatchEnv
+from .environment import MultiAgentConstrainEnv, MultiAgentEnv, MultiAgentGraphConstrainEnv
+from .make_env import make_env
+from . import distributed
+
+__version__ = "0.1.0"
+__all__ = ["EnvConfig", "GpuBatchEnv", "MultiAgentEnv", "MultiAgentConstrainEnv",
+           "MultiAgentGraphConstrainEnv", "make_env", "distributed"]

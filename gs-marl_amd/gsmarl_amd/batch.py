@@ -1,0 +1,193 @@
+"""GpuBatchEnv — B independent MultiAgentGraphConstrainEnv instances resident
+in HBM, stepped by the HIP kernels in libgsm.so.
+
+State and outputs are PyTorch device tensors (PyTorch is the allocator and
+stream provider only); every compute call goes through the C ABI. Layout
+(SoA over envs):
+
+    pos        [B, E, 2] f32   agents [0,N), goals [N,2N), obstacles [2N,E)
+    vel        [B, N, 2] f32
+    node_feat  [B, E, 7] f32   vx vy px py gx-px gy-py type
+    obs        [B, N, 6]       = node_feat[:, :N, :6]  (a view: MPE obs order)
+    reward     [B, N] f32, cost [B, N] f32 (exact counts), done [B] u8
+    edge_ptr   [B+1] i64; edge_index [2, cap] i32 (global node ids b*E+e),
+    edge_attr  [cap] f32 (distance); valid prefix = edge_ptr[B]
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional
+
+import torch
+
+from . import _lib
+from .config import EnvConfig
+
+
+def _require_gpu(device) -> torch.device:
+    device = torch.device(device)
+    if device.type != "cuda" or not torch.cuda.is_available():
+        raise _lib.GsmError("GpuBatchEnv needs a ROCm GPU (torch.cuda.is_available() is False); "
+                            "there is no CPU fallback by design")
+    return device
+
+
+class GpuBatchEnv:
+    """Batched navigation env; ``step``/``reset`` are asynchronous on the
+    current torch stream and return dicts of device tensors."""
+
+    def __init__(self, cfg: EnvConfig, device="cuda"):
+        self.cfg = cfg
+        self.device = _require_gpu(device)
+        self.lib = _lib.load()
+        self.sizes = _lib.query_sizes(cfg, self.lib)
+        self._ccfg = _lib.make_config(cfg)
+        h = C.c_void_p()
+        _lib.check(self.lib, self.lib.gsm_create(C.byref(self._ccfg), C.byref(h)), None, "gsm_create")
+        self._h = h
+        B, N, E = cfg.n_envs, cfg.n_agents, self.sizes.n_entities
+        self.B, self.N, self.E = B, N, E
+        dev = self.device
+        f32, i32 = torch.float32, torch.int32
+        cap = int(self.sizes.edge_capacity)
+        self.t = dict(
+            pos=torch.zeros(B, E, 2, dtype=f32, device=dev),
+            vel=torch.zeros(B, N, 2, dtype=f32, device=dev),
+            step_count=torch.zeros(B, dtype=i32, device=dev),
+            episode=torch.full((B,), -1, dtype=i32, device=dev),
+            ep_acc=torch.zeros(B, 2, dtype=f32, device=dev),
+            ep_last=torch.zeros(B, 2, dtype=f32, device=dev),
+            node_feat=torch.zeros(B, E, 7, dtype=f32, device=dev),
+            reward=torch.zeros(B, N, dtype=f32, device=dev),
+            cost=torch.zeros(B, N, dtype=f32, device=dev),
+            done=torch.zeros(B, dtype=torch.uint8, device=dev),
+            edge_count=torch.zeros(B, dtype=i32, device=dev),
+            block_edge_sum=torch.zeros(self.sizes.n_blocks, dtype=i32, device=dev),
+            edge_ptr=torch.zeros(B + 1, dtype=torch.int64, device=dev),
+            edge_index=torch.zeros(2, cap, dtype=i32, device=dev),
+            edge_attr=torch.zeros(cap, dtype=f32, device=dev),
+        )
+        bufs = _lib.GsmBuffers(**{k: self.t[k].data_ptr() for k in _lib.BUFFER_FIELDS})
+        _lib.check(self.lib, self.lib.gsm_bind(self._h, C.byref(bufs)), self._h, "gsm_bind")
+        self.agent_id = torch.arange(N, dtype=torch.int64, device=dev).expand(B, N)
+        self._graph_actions = {}
+
+    # ------------------------------------------------------------------ utils
+    def _stream(self):
+        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+
+    def _chk(self, rc, what):
+        _lib.check(self.lib, rc, self._h, what)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            self.lib.gsm_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --------------------------------------------------------------- outputs
+    def outputs(self, sync_edges: bool = True) -> dict:
+        t = self.t
+        out = dict(obs=t["node_feat"][:, : self.N, :6], node_feat=t["node_feat"],
+                   agent_id=self.agent_id, reward=t["reward"], cost=t["cost"], done=t["done"],
+                   edge_ptr=t["edge_ptr"])
+        if sync_edges:
+            total = int(t["edge_ptr"][self.B].item())
+            out["edge_index"] = t["edge_index"][:, :total]
+            out["edge_attr"] = t["edge_attr"][:total]
+        else:
+            out["edge_index"] = t["edge_index"]
+            out["edge_attr"] = t["edge_attr"]
+        return out
+
+    # ------------------------------------------------------------------- API
+    def reset(self, seed: Optional[int] = None, env_mask: Optional[torch.Tensor] = None,
+              sync_edges: bool = True) -> dict:
+        """Re-lay-out the masked envs (all if None). With ``seed`` the episode
+        counters restart and ``seed`` keys every later layout."""
+        mask_ptr = None
+        if env_mask is not None:
+            env_mask = env_mask.to(device=self.device, dtype=torch.uint8).contiguous()
+            if env_mask.numel() != self.B:
+                raise ValueError("env_mask must have n_envs elements")
+            mask_ptr = C.c_void_p(env_mask.data_ptr())
+        reseed = seed is not None
+        if reseed:
+            self.cfg.seed = int(seed)
+        s = int(seed) & 0xFFFFFFFFFFFFFFFF if reseed else 0
+        self._chk(self.lib.gsm_reset(self._h, s, int(reseed), mask_ptr, self._stream()), "gsm_reset")
+        return self.outputs(sync_edges)
+
+    def _action_fmt(self, actions: torch.Tensor) -> int:
+        B, N = self.B, self.N
+        if actions.device != self.device:
+            raise ValueError("actions must be on the env's device")
+        if actions.dtype == torch.int32 and tuple(actions.shape) == (B, N):
+            return _lib.ACT_INDEX
+        if actions.dtype == torch.float32 and tuple(actions.shape) == (B, N, 5):
+            return _lib.ACT_ONEHOT
+        if actions.dtype == torch.float32 and tuple(actions.shape) == (B, N, 2):
+            return _lib.ACT_CONT
+        raise ValueError(f"actions must be int32 [B,N], float32 one-hot [B,N,5] or float32 [B,N,2]; "
+                         f"got {actions.dtype} {tuple(actions.shape)}")
+
+    def step(self, actions: torch.Tensor, sync_edges: bool = True) -> dict:
+        if not actions.is_contiguous():
+            actions = actions.contiguous()
+        fmt = self._action_fmt(actions)
+        self._chk(self.lib.gsm_step(self._h, C.c_void_p(actions.data_ptr()), fmt, self._stream()),
+                  "gsm_step")
+        return self.outputs(sync_edges)
+
+    def observe(self, sync_edges: bool = True) -> dict:
+        self._chk(self.lib.gsm_observe(self._h, self._stream()), "gsm_observe")
+        return self.outputs(sync_edges)
+
+    # ------------------------------------------------- checkpoint / injection
+    STATE_KEYS = ("pos", "vel", "step_count", "episode", "ep_acc", "ep_last")
+
+    def get_state(self) -> dict:
+        return {k: self.t[k].clone() for k in self.STATE_KEYS}
+
+    def set_state(self, state: dict, observe: bool = True) -> Optional[dict]:
+        for k, v in state.items():
+            if k not in self.STATE_KEYS:
+                raise KeyError(k)
+            self.t[k].copy_(torch.as_tensor(v).to(self.t[k].dtype))
+        return self.observe() if observe else None
+
+    # ------------------------------------------------------------ HIP graph
+    def capture(self, actions_seq: torch.Tensor, n_steps: int, timing: bool = False, slot: int = 0) -> None:
+        """Capture ``n_steps`` steps into HIP graph ``slot``; the j-th captured
+        step uses ``actions_seq[j % len(actions_seq)]`` (a [T, B, N(,k)] device tensor)."""
+        a = actions_seq.contiguous()
+        fmt = self._action_fmt(a[0])
+        stride = a[0].numel() * a.element_size()
+        self._graph_actions[slot] = a   # keep alive while the graph exists
+        self._chk(self.lib.gsm_graph_capture(self._h, int(slot), C.c_void_p(a.data_ptr()), stride,
+                                             a.shape[0], int(n_steps), fmt, int(timing)),
+                  "gsm_graph_capture")
+
+    def replay(self, slot: int = 0) -> None:
+        self._chk(self.lib.gsm_graph_launch(self._h, int(slot), self._stream()), "gsm_graph_launch")
+
+    def graph_kernel_ms(self, slot: int = 0):
+        """(mean step-kernel ms, mean edge-emit-kernel ms) of the last timed replay."""
+        a, b = C.c_float(), C.c_float()
+        self._chk(self.lib.gsm_graph_kernel_ms(self._h, int(slot), C.byref(a), C.byref(b)),
+                  "gsm_graph_kernel_ms")
+        return a.value, b.value
+
+    # ---------------------------------------------------------------- metrics
+    def episode_metrics(self) -> torch.Tensor:
+        """[sum of last-episode rewards, sum of last-episode costs, finished
+        episodes] over this shard (float64, on device) — the vector the
+        distributed runner all-reduces (gsmarl_amd.distributed)."""
+        ep = self.t["episode"].to(torch.float64).clamp_min(0).sum()
+        s = self.t["ep_last"].to(torch.float64).sum(0)
+        return torch.stack([s[0], s[1], ep])

@@ -1,0 +1,165 @@
+/*
+ * gsm.h — C ABI of libgsm.so, the MI355X (gfx950) batched step path of
+ * GS-MARL's MultiAgentGraphConstrainEnv.
+ *
+ * Drop-in boundary. The reference has no FFI: its boundary is the Python
+ * env classes in gsmarl/envs/mpe_env/multiagent/environment.py
+ * (/root/reference/GSMARL.egg-info/SOURCES.txt:15; contracts at
+ * /root/reference/readme.md:29-41), constructed by make_env.py
+ * (SOURCES.txt:12) and called from the vec-env workers (SOURCES.txt:11).
+ * The reference sources are absent (readme.md:1), so each entry point below
+ * cites the reference interface it replaces at the granularity available.
+ * The binding a maintainer adds on the reference side (ctypes) is shown in
+ * INTEGRATION.md; the in-tree binding is gs-marl_amd/gsmarl_amd/_lib.py.
+ *
+ * Rules of the ABI:
+ *  - plain C types only; pointers to device memory are owned by the caller
+ *    (PyTorch allocates them) and merely borrowed by the library;
+ *  - nothing is allocated and nothing synchronises inside gsm_step /
+ *    gsm_reset / gsm_observe, so they can be captured into a HIP graph;
+ *  - every call returns GSM_OK (0) or a negative gsm_status; no C++
+ *    exception crosses the boundary; gsm_last_error() has the message;
+ *  - a handle is used from one host thread at a time (the GIL serialises);
+ *  - `stream` is a hipStream_t passed as void* (NULL = legacy default).
+ */
+#ifndef GSM_H_
+#define GSM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GSM_ABI_VERSION 1
+
+typedef enum gsm_status {
+    GSM_OK = 0,
+    GSM_EINVAL = -1,   /* bad argument / config                        */
+    GSM_EHIP = -2,     /* HIP runtime error (message has hipError_t)    */
+    GSM_ESTATE = -3,   /* call out of order (e.g. step before bind)     */
+} gsm_status;
+
+typedef enum gsm_scenario {
+    GSM_SCEN_NAVIGATION = 0,   /* scenarios/exp1.py|exp2.py (SOURCES.txt:21-22) */
+} gsm_scenario;
+
+typedef enum gsm_action_fmt {
+    GSM_ACT_ONEHOT = 0,   /* float32 [B][N][5]; u = [a1-a2, a3-a4] (MPE discrete_action_space) */
+    GSM_ACT_INDEX = 1,    /* int32   [B][N];    same mapping as the one-hot of the index        */
+    GSM_ACT_CONT = 2,     /* float32 [B][N][2]; u = a (continuous)                              */
+} gsm_action_fmt;
+
+/* Launch modes of the step kernel (gsm_observe / gsm_reset reuse it). */
+typedef enum gsm_mode {
+    GSM_MODE_STEP = 0,
+    GSM_MODE_RESET = 1,
+    GSM_MODE_OBSERVE = 2,
+} gsm_mode;
+
+/* Environment configuration; mirrors gsmarl_amd.config.EnvConfig 1:1.
+ * Replaces the env part of gsmarl/config.py (SOURCES.txt:7, readme.md:47)
+ * and the constants of core.py / the scenario files. */
+typedef struct gsm_config {
+    int32_t abi_version;      /* = GSM_ABI_VERSION                           */
+    int32_t scenario;         /* gsm_scenario                                */
+    int32_t n_envs;           /* B: env instances held by this handle        */
+    int32_t n_agents;         /* N (goals = N)                               */
+    int32_t n_obstacles;      /* No                                          */
+    int32_t episode_length;   /* readme.md:101 -> 100                        */
+    int32_t auto_reset;       /* reset an env in-kernel when its episode ends */
+    int32_t shared_reward;    /* every agent gets the sum of rewards         */
+    int64_t env_base;         /* global id of env 0 (sharding; Philox key)   */
+    uint64_t seed;
+    float dt, damping, mass, contact_force, contact_margin, sensitivity;
+    float max_speed;          /* <= 0: no clamp (MPE max_speed = None)       */
+    float world_half;         /* L: layout box is [-L, L]^2                  */
+    float agent_size, goal_size, obstacle_size;
+    float sense_radius;       /* R: graph edge radius                        */
+    float contact_cutoff;     /* skip pair force when d - dmin > cutoff*k     */
+} gsm_config;
+
+/* Sizes the caller must allocate (gsm_query_sizes). */
+typedef struct gsm_sizes {
+    int32_t n_entities;       /* E = 2N + No                                 */
+    int32_t node_feat_dim;    /* 7                                           */
+    int32_t obs_dim;          /* 6                                           */
+    int32_t envs_per_block;   /* envs handled by one step-kernel workgroup   */
+    int32_t n_blocks;         /* length of block_edge_sum                    */
+    int32_t max_edges_per_env;
+    int64_t edge_capacity;    /* length of edge_attr and of each edge_index row */
+} gsm_sizes;
+
+/* Caller-owned device buffers (all contiguous, row-major). */
+typedef struct gsm_buffers {
+    /* state */
+    float *pos;               /* [B][E][2]   agents, goals, obstacles         */
+    float *vel;               /* [B][N][2]   agents only (landmarks immovable) */
+    int32_t *step_count;      /* [B]         steps since reset                */
+    int32_t *episode;         /* [B]         episode index (-1 before reset)  */
+    float *ep_acc;            /* [B][2]      running (sum reward, sum cost)   */
+    float *ep_last;           /* [B][2]      totals of the last finished episode */
+    /* outputs of the last reset/step/observe */
+    float *node_feat;         /* [B][E][7]   vx vy px py gx-px gy-py type     */
+    float *reward;            /* [B][N]                                       */
+    float *cost;              /* [B][N]      collision counts (exact ints)    */
+    uint8_t *done;            /* [B]                                          */
+    int32_t *edge_count;      /* [B]                                          */
+    int32_t *block_edge_sum;  /* [n_blocks]  scratch                          */
+    int64_t *edge_ptr;        /* [B+1]       CSR offsets into edge arrays     */
+    int32_t *edge_index;      /* [2][edge_capacity] global node ids (b*E+e)   */
+    float *edge_attr;         /* [edge_capacity]    distance                  */
+} gsm_buffers;
+
+typedef struct gsm_handle gsm_handle;
+
+int gsm_abi_version(void);
+
+/* Validates cfg and fills sizes. Host-only, no HIP call. */
+int gsm_query_sizes(const gsm_config *cfg, gsm_sizes *out);
+
+/* Replaces make_env(scenario) -> MultiAgentGraphConstrainEnv(world, ...)
+ * (make_env.py, SOURCES.txt:12; environment.py, SOURCES.txt:15). Host-only. */
+int gsm_create(const gsm_config *cfg, gsm_handle **out);
+
+/* Borrow caller-allocated device buffers (sizes from gsm_query_sizes). */
+int gsm_bind(gsm_handle *h, const gsm_buffers *bufs);
+
+/* Replaces env.reset() -> scenario.reset_world(world) (environment.py /
+ * scenario.py, SOURCES.txt:15,19). reseed != 0: episode counters restart
+ * and `seed` becomes the layout key. env_mask: device uint8 [B] or NULL
+ * (= all envs). Outputs are recomputed for every env. */
+int gsm_reset(gsm_handle *h, uint64_t seed, int reseed, const uint8_t *env_mask, void *stream);
+
+/* Replaces env.step(action_n) (environment.py, SOURCES.txt:15): _set_action,
+ * world.step() (core.py, SOURCES.txt:14), reward/cost/done callbacks and the
+ * graph observation, for all B envs. actions: device pointer in action_fmt. */
+int gsm_step(gsm_handle *h, const void *actions, int action_fmt, void *stream);
+
+/* Recompute every output for the current state (after the caller rewrote
+ * state buffers, e.g. set_state). */
+int gsm_observe(gsm_handle *h, void *stream);
+
+/* Capture n_steps gsm_step launches into HIP graph `slot` (0..GSM_GRAPH_SLOTS-1;
+ * actions for the j-th captured step at actions + (j % n_actions) *
+ * action_stride_bytes). with_timing != 0 brackets each step kernel and each
+ * edge-emit kernel with HIP event records (read by gsm_graph_kernel_ms).
+ * Graphs are dropped by gsm_bind and by a reseed to a different seed. */
+#define GSM_GRAPH_SLOTS 4
+int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t action_stride_bytes,
+                      int32_t n_actions, int32_t n_steps, int action_fmt, int with_timing);
+int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream);
+/* After a timed launch of `slot` has completed: mean duration (ms) of the
+ * step kernel and of the edge-emit kernel over the captured steps. */
+int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_mean_ms, float *emit_mean_ms);
+
+int gsm_destroy(gsm_handle *h);
+
+/* Copies the last error message of h (or of the library when h == NULL). */
+int gsm_last_error(const gsm_handle *h, char *buf, size_t len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GSM_H_ */

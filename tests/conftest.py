@@ -1,0 +1,43 @@
+import sys
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parents[1]
+for p in (ROOT, ROOT / "gs-marl_amd"):
+    if str(p) not in sys.path:
+        sys.path.insert(0, str(p))
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a ROCm GPU (MI355X); run with -m gpu")
+
+
+def gpu_available() -> bool:
+    try:
+        import torch
+        return torch.cuda.is_available()
+    except Exception:
+        return False
+
+
+@pytest.fixture(scope="session")
+def ocfg_factory():
+    """Build an oracle config from product EnvConfig kwargs."""
+    from oracle import batch_ref as br
+
+    def make(**kw):
+        return br.make_cfg(**kw)
+    return make
+
+
+def pytest_collection_modifyitems(config, items):
+    """GPU tests skip (not fail) on a machine without a GPU, unless
+    GSM_REQUIRE_GPU=1 demands one (the GPU box runs them with -m gpu)."""
+    import os
+    if gpu_available() or os.environ.get("GSM_REQUIRE_GPU") == "1":
+        return
+    skip = pytest.mark.skip(reason="no ROCm GPU visible")
+    for it in items:
+        if "gpu" in it.keywords:
+            it.add_marker(skip)
