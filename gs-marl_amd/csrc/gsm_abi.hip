@@ -26,7 +26,7 @@ struct gsm_handle {
     struct Slot {
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
-        std::vector<hipEvent_t> events;   // 3 per step when timing
+        std::vector<hipEvent_t> events;   // 2 per step + 1 when timing
         int steps = 0;
     } slots[GSM_GRAPH_SLOTS];
 };
@@ -268,35 +268,68 @@ int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t 
         e = hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking);
         if (e != hipSuccess) return hip_fail(h, e, "hipStreamCreate");
     }
+    // The graph is built node by node (a linear chain) rather than by stream
+    // capture: event-record nodes for per-kernel timing are then explicit
+    // (the capture path of the HIP runtime bundled with PyTorch rejects
+    // hipEventRecordWithFlags(..., hipEventRecordExternal)).
+    //   [E0] -> step_0 -> [E1] -> emit_0 -> [E2] -> step_1 -> ...
     if (with_timing) {
-        sl.events.resize(3 * (size_t)n_steps, nullptr);
+        sl.events.resize(2 * (size_t)n_steps + 1, nullptr);
         for (auto &ev : sl.events) {
             e = hipEventCreate(&ev);
             if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipEventCreate"); }
         }
     }
-    e = hipStreamBeginCapture(h->cap_stream, hipStreamCaptureModeThreadLocal);
-    if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipStreamBeginCapture"); }
+    e = hipGraphCreate(&sl.graph, 0);
+    if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipGraphCreate"); }
     gsm::DevParams p = h->dp;
     p.mode = GSM_MODE_STEP;
     p.action_fmt = action_fmt;
     p.env_mask = nullptr;
     p.reseed = 0;
-    hipError_t first = hipSuccess;
-    for (int t = 0; t < n_steps && first == hipSuccess; ++t) {
+    hipGraphNode_t prev = nullptr;
+    const char *what = "";
+    int at = 0;
+    auto add_event = [&](int k) -> hipError_t {
+        if (!with_timing) return hipSuccess;
+        hipGraphNode_t n;
+        const hipError_t r = hipGraphAddEventRecordNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0,
+                                                        sl.events[k]);
+        if (r == hipSuccess) prev = n;
+        return r;
+    };
+    auto add_kernel = [&](const void *fn, size_t lds) -> hipError_t {
+        hipKernelNodeParams kp = {};
+        void *args[] = {&p};
+        kp.func = const_cast<void *>(fn);
+        kp.gridDim = dim3(gsm::grid_blocks(p));
+        kp.blockDim = dim3(gsm::kBlock);
+        kp.sharedMemBytes = (unsigned)lds;
+        kp.kernelParams = args;
+        kp.extra = nullptr;
+        hipGraphNode_t n;
+        const hipError_t r = hipGraphAddKernelNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0, &kp);
+        if (r == hipSuccess) prev = n;
+        return r;
+    };
+    what = "event node";
+    e = add_event(0);
+    for (int t = 0; t < n_steps && e == hipSuccess; ++t) {
+        at = t;
         p.actions = (const char *)actions + (int64_t)(t % n_actions) * stride;
-        if (with_timing) first = hipEventRecord(sl.events[3 * t], h->cap_stream);
-        if (first == hipSuccess) first = gsm::launch_step_kernel(p, h->cap_stream);
-        if (with_timing && first == hipSuccess) first = hipEventRecord(sl.events[3 * t + 1], h->cap_stream);
-        if (first == hipSuccess) first = gsm::launch_emit_kernel(p, h->cap_stream);
-        if (with_timing && first == hipSuccess) first = hipEventRecord(sl.events[3 * t + 2], h->cap_stream);
+        what = "step kernel node";
+        e = add_kernel(gsm::step_kernel_fn(), gsm::step_kernel_lds(p));
+        if (e == hipSuccess) { what = "event node"; e = add_event(2 * t + 1); }
+        if (e == hipSuccess) { what = "emit kernel node"; e = add_kernel(gsm::emit_kernel_fn(), gsm::emit_kernel_lds(p)); }
+        if (e == hipSuccess) { what = "event node"; e = add_event(2 * t + 2); }
     }
-    hipGraph_t g = nullptr;
-    e = hipStreamEndCapture(h->cap_stream, &g);
-    if (first != hipSuccess) { if (g) (void)hipGraphDestroy(g); drop_slot(sl); return hip_fail(h, first, "capture"); }
-    if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipStreamEndCapture"); }
-    sl.graph = g;
-    e = hipGraphInstantiate(&sl.exec, g, nullptr, nullptr, 0);
+    if (e != hipSuccess) {
+        drop_slot(sl);
+        char where[96];
+        snprintf(where, sizeof where, "graph build (step %d, %s)", at, what);
+        return hip_fail(h, e, where);
+    }
+    e = hipGraphInstantiate(&sl.exec, sl.graph, nullptr, nullptr, 0);
     if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipGraphInstantiate"); }
     e = hipGraphUpload(sl.exec, h->cap_stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->cap_stream);
@@ -322,8 +355,8 @@ int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_ms, float *emit
     double a = 0, b = 0;
     for (int t = 0; t < sl.steps; ++t) {
         float x = 0, y = 0;
-        hipError_t e = hipEventElapsedTime(&x, sl.events[3 * t], sl.events[3 * t + 1]);
-        if (e == hipSuccess) e = hipEventElapsedTime(&y, sl.events[3 * t + 1], sl.events[3 * t + 2]);
+        hipError_t e = hipEventElapsedTime(&x, sl.events[2 * t], sl.events[2 * t + 1]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&y, sl.events[2 * t + 1], sl.events[2 * t + 2]);
         if (e != hipSuccess) return hip_fail(h, e, "hipEventElapsedTime");
         a += x;
         b += y;

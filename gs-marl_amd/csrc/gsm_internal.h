@@ -38,6 +38,12 @@ struct DevParams {
 // Launch the step kernel (physics / reset / observe by p.mode) and the edge
 // emitter for all B envs on `s`. Returns the first hipError_t.
 hipError_t launch_step(const DevParams &p, hipStream_t s);
+// for explicit graph construction (kernel nodes)
+int grid_blocks(const DevParams &p);
+const void *step_kernel_fn();
+const void *emit_kernel_fn();
+size_t step_kernel_lds(const DevParams &p);
+size_t emit_kernel_lds(const DevParams &p);
 hipError_t launch_step_kernel(const DevParams &p, hipStream_t s);
 hipError_t launch_emit_kernel(const DevParams &p, hipStream_t s);
 

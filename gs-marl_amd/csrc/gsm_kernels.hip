@@ -323,7 +323,7 @@ __device__ void env_emit(const DevParams &p, const int b, const int lane, int64_
     const int32_t g0 = (int32_t)(eb * E);
 
     // agent rows: candidates agents [0,N), own goal, obstacles (entity order)
-    const int KA = 2 * N + 1;
+    const int KA = N + 1 + No;
     for (int i = 0; i < N; ++i) {
         const float2 a = s_pos[i];
         for (int c0 = 0; c0 < KA; c0 += kWave) {
@@ -397,17 +397,21 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_edges_kernel(DevParams p) {
     env_emit(p, b, lane, off, smem + wave * p.wave_lds_emit);
 }
 
+int grid_blocks(const DevParams &p) { return (p.B + kWavesPerBlock - 1) / kWavesPerBlock; }
+const void *step_kernel_fn() { return reinterpret_cast<const void *>(&gsm_step_kernel); }
+const void *emit_kernel_fn() { return reinterpret_cast<const void *>(&gsm_emit_edges_kernel); }
+size_t step_kernel_lds(const DevParams &p) { return (size_t)kWavesPerBlock * p.wave_lds_step + 16; }
+size_t emit_kernel_lds(const DevParams &p) { return (size_t)kWavesPerBlock * p.wave_lds_emit + 8 * kWavesPerBlock; }
+
 hipError_t launch_step_kernel(const DevParams &p, hipStream_t s) {
-    const int nblk = (p.B + kWavesPerBlock - 1) / kWavesPerBlock;
-    const size_t lds = (size_t)kWavesPerBlock * p.wave_lds_step + 16;
-    hipLaunchKernelGGL(gsm_step_kernel, dim3(nblk), dim3(kBlock), lds, s, p);
+    (void)hipGetLastError();   // report this launch's error only
+    hipLaunchKernelGGL(gsm_step_kernel, dim3(grid_blocks(p)), dim3(kBlock), step_kernel_lds(p), s, p);
     return hipGetLastError();
 }
 
 hipError_t launch_emit_kernel(const DevParams &p, hipStream_t s) {
-    const int nblk = (p.B + kWavesPerBlock - 1) / kWavesPerBlock;
-    const size_t lds = (size_t)kWavesPerBlock * p.wave_lds_emit + 8 * kWavesPerBlock;
-    hipLaunchKernelGGL(gsm_emit_edges_kernel, dim3(nblk), dim3(kBlock), lds, s, p);
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(gsm_emit_edges_kernel, dim3(grid_blocks(p)), dim3(kBlock), emit_kernel_lds(p), s, p);
     return hipGetLastError();
 }
 

@@ -207,11 +207,20 @@ def test_episode_rollout_stepwise(N, B):
         assert np.array_equal(_np(env.t["episode"]), nst["episode"])
         assert_state_close(_np(env.t["pos"]), nst["pos"], f"pos t={t}")
         assert_state_close(_np(env.t["vel"]), nst["vel"], f"vel t={t}")
+        # episode accounting from the kernel's own per-step outputs
+        acc_exp = st["ep_acc"].astype(np.float64) + np.stack(
+            [_np(out["reward"]).astype(np.float64).sum(-1), _np(out["cost"]).astype(np.float64).sum(-1)], -1)
         if done.any():    # re-laid-out envs are bit-exact
             lay = br.layout(ocfg, np.nonzero(done)[0], nst["episode"][done], 7)
             assert np.array_equal(_np(env.t["pos"])[done], lay)
-            assert np.allclose(_np(env.t["ep_last"])[done], nst["ep_last"][done], rtol=1e-5, atol=1e-4)
-        assert np.allclose(_np(env.t["ep_acc"]), nst["ep_acc"], rtol=1e-5, atol=1e-4)
+            assert np.allclose(_np(env.t["ep_last"])[done], acc_exp[done], rtol=1e-5, atol=1e-4)
+            acc_exp[done] = 0
+        assert np.allclose(_np(env.t["ep_acc"]), acc_exp, rtol=1e-5, atol=1e-4)
+        # cost exact (fp32 predicate) on the post-physics state of envs that did not reset
+        keep = ~done
+        if keep.any():
+            _, c32 = br.reward_cost(ocfg, _np(env.t["pos"])[keep], np.float32)
+            assert np.array_equal(_np(out["cost"])[keep], c32)
         check_outputs(env, ocfg, out)
         assert np.allclose(_np(out["reward"]), ob["reward"], rtol=3e-7, atol=2e-6)
 
