@@ -73,13 +73,27 @@ int check_config(const gsm_config *c, std::string *why) {
     return GSM_OK;
 }
 
+// kernel family and envs per wave for a config
+void choose_path(int M, int *path, int *G) {
+    if (M <= gsm::kWave) {
+        *path = gsm::kPathSeg;
+        int g = gsm::kWave / M;
+        *G = g > gsm::kMaxSegEnvsPerWave ? gsm::kMaxSegEnvsPerWave : g;
+    } else {
+        *path = gsm::kPathGeneric;
+        *G = 1;
+    }
+}
+
 void fill_sizes(const gsm_config *c, gsm_sizes *s) {
     const int N = c->n_agents, No = c->n_obstacles, M = N + No;
+    int path, G;
+    choose_path(M, &path, &G);
     s->n_entities = 2 * N + No;
     s->node_feat_dim = 7;
     s->obs_dim = 6;
-    s->envs_per_block = gsm::kWavesPerBlock;
-    s->n_blocks = (c->n_envs + gsm::kWavesPerBlock - 1) / gsm::kWavesPerBlock;
+    s->envs_per_block = gsm::kWavesPerBlock * G;
+    s->n_blocks = (c->n_envs + s->envs_per_block - 1) / s->envs_per_block;
     s->max_edges_per_env = M * (M - 1) + 2 * N;
     s->edge_capacity = (int64_t)c->n_envs * s->max_edges_per_env;
 }
@@ -93,7 +107,8 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
     p->No = No;
     p->E = 2 * N + No;
     p->M = N + No;
-    // slices per agent so that N*S lanes of the wave share the contact loop
+    choose_path(p->M, &p->path, &p->G);
+    // generic path: N*S lanes of the wave share the contact loop
     int S = N <= gsm::kWave ? gsm::kWave / N : 1;
     if (S > p->M) S = p->M;
     if (S < 1) S = 1;
@@ -104,14 +119,21 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
     p->seed_lo = (uint32_t)(c->seed & 0xFFFFFFFFull);
     p->seed_hi = (uint32_t)(c->seed >> 32);
     p->env_base = c->env_base;
-    p->wave_lds_step = align16(8 * p->E + 8 * N + 12 * S * N);
-    p->wave_lds_emit = align16(8 * p->E);
+    if (p->path == gsm::kPathSeg) {
+        // positions + staged node-feature rows of the wave's G envs
+        p->wave_lds_step = align16(8 * p->G * p->E + 28 * p->G * p->E);
+        p->wave_lds_emit = align16(8 * p->G * p->E);
+    } else {
+        p->wave_lds_step = align16(8 * p->E + 8 * N + 12 * S * N);
+        p->wave_lds_emit = align16(8 * p->E);
+    }
     const float L = c->world_half;
     p->L = L;
     p->twoL = L * 2.0f;
     p->dt = c->dt;
     p->omd = 1.0f - c->damping;
     p->mass = c->mass;
+    p->inv_mass = 1.0f / c->mass;
     p->cf = c->contact_force;
     p->k = c->contact_margin;
     p->inv_k = 1.0f / c->contact_margin;
@@ -208,7 +230,8 @@ int gsm_bind(gsm_handle *h, const gsm_buffers *b) {
     if (!b) return fail(h, GSM_EINVAL, "buffers is NULL");
     const void *req[] = {b->pos, b->vel, b->step_count, b->episode, b->ep_acc, b->ep_last,
                          b->node_feat, b->reward, b->cost, b->done, b->edge_count,
-                         b->block_edge_sum, b->edge_ptr, b->edge_index, b->edge_attr};
+                         b->block_edge_sum, b->edge_ptr, b->edge_index, b->edge_attr,
+                         b->row_mask, b->contact_mask};
     for (const void *q : req)
         if (!q) return fail(h, GSM_EINVAL, "a required buffer pointer is NULL");
     if (((uintptr_t)b->pos | (uintptr_t)b->vel | (uintptr_t)b->ep_acc | (uintptr_t)b->ep_last) & 7)
@@ -229,6 +252,8 @@ int gsm_bind(gsm_handle *h, const gsm_buffers *b) {
     p.edge_ptr = b->edge_ptr;
     p.edge_index = b->edge_index;
     p.edge_attr = b->edge_attr;
+    p.row_mask = b->row_mask;
+    p.contact_mask = b->contact_mask;
     h->bound = true;
     drop_graph(h);   // a captured graph holds the old pointers
     return GSM_OK;
@@ -318,9 +343,9 @@ int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t 
         at = t;
         p.actions = (const char *)actions + (int64_t)(t % n_actions) * stride;
         what = "step kernel node";
-        e = add_kernel(gsm::step_kernel_fn(), gsm::step_kernel_lds(p));
+        e = add_kernel(gsm::step_kernel_fn(p), gsm::step_kernel_lds(p));
         if (e == hipSuccess) { what = "event node"; e = add_event(2 * t + 1); }
-        if (e == hipSuccess) { what = "emit kernel node"; e = add_kernel(gsm::emit_kernel_fn(), gsm::emit_kernel_lds(p)); }
+        if (e == hipSuccess) { what = "emit kernel node"; e = add_kernel(gsm::emit_kernel_fn(p), gsm::emit_kernel_lds(p)); }
         if (e == hipSuccess) { what = "event node"; e = add_event(2 * t + 2); }
     }
     if (e != hipSuccess) {
@@ -363,6 +388,13 @@ int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_ms, float *emit
     }
     if (step_ms) *step_ms = (float)(a / sl.steps);
     if (emit_ms) *emit_ms = (float)(b / sl.steps);
+    return GSM_OK;
+}
+
+int gsm_debug_set_stamps(gsm_handle *h, void *stamps) {
+    if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
+    h->dp.stamps = (uint64_t *)stamps;
+    drop_graph(h);
     return GSM_OK;
 }
 

@@ -1,0 +1,147 @@
+// Device helpers shared by the generic and the segmented kernel families.
+#pragma once
+#include "gsm_internal.h"
+#include "gsm_philox.h"
+
+namespace gsm {
+
+enum { kModeStep = 0, kModeReset = 1, kModeObserve = 2 };
+
+// v_writelane_b32: replace lane `lane` of `old` with the wave-uniform `src`
+// (the LLVM intrinsic has no clang builtin; bound by name so the compiler
+// still schedules it and resolves its hazards)
+__device__ uint32_t writelane_u32(uint32_t src, uint32_t lane, uint32_t old) __asm("llvm.amdgcn.writelane.i32");
+
+// Orders LDS traffic between the lanes of one wave: LDS ops of a wave execute
+// in order, so only compiler motion has to be fenced.
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ int wave_sum(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+// --- DPP wave collectives (gfx9 DPP: quad_perm, row mirrors, row_shr, row_bcast)
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, kCtrl, kRowMask, 0xf, true);
+}
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), kCtrl, kRowMask, 0xf, true));
+}
+// sum over the 64 lanes, returned wave-uniform
+__device__ __forceinline__ int wave_total(int v) {
+    v += dpp_i<0xB1>(v);          // quad_perm [1,0,3,2]
+    v += dpp_i<0x4E>(v);          // quad_perm [2,3,0,1]
+    v += dpp_i<0x141>(v);         // row_half_mirror
+    v += dpp_i<0x140>(v);         // row_mirror: every lane holds its row's sum
+    v += dpp_i<0x142, 0xa>(v);    // row_bcast:15 -> rows 1, 3
+    v += dpp_i<0x143, 0xc>(v);    // row_bcast:31 -> rows 2, 3 (lane 63 = total)
+    return __builtin_amdgcn_readlane(v, 63);
+}
+__device__ __forceinline__ float wave_total(float v) {
+    v += dpp_f<0xB1>(v);
+    v += dpp_f<0x4E>(v);
+    v += dpp_f<0x141>(v);
+    v += dpp_f<0x140>(v);
+    v += dpp_f<0x142, 0xa>(v);
+    v += dpp_f<0x143, 0xc>(v);
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+// inclusive scan over the 64 lanes (Hillis-Steele in rows of 16, then row broadcasts)
+__device__ __forceinline__ int wave_scan(int v) {
+    v += dpp_i<0x111>(v);         // row_shr:1
+    v += dpp_i<0x112>(v);         // row_shr:2
+    v += dpp_i<0x114>(v);         // row_shr:4
+    v += dpp_i<0x118>(v);         // row_shr:8
+    v += dpp_i<0x142, 0xa>(v);
+    v += dpp_i<0x143, 0xc>(v);
+    return v;
+}
+
+// In-kernel phase stamps for diagnostic builds (-DGSM_STAMPS): lane 0 of each
+// wave records s_memtime at phase boundaries into p.stamps[wave][k]. Never
+// compiled into the product library.
+#ifdef GSM_STAMPS
+#define GSM_STAMP(p, wave_id, k)                                                                  \
+    do {                                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        unsigned long long t_;                                                                    \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");               \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        if ((p).stamps && (threadIdx.x & 63) == 0) (p).stamps[(int64_t)(wave_id)*16 + (k)] = t_;  \
+    } while (0)
+#define GSM_RSTAMP(p, wave_id, k)                                                                 \
+    do {                                                                                          \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        unsigned long long t_;                                                                    \
+        asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");           \
+        __builtin_amdgcn_sched_barrier(0);                                                        \
+        if ((p).stamps && (threadIdx.x & 63) == 0) (p).stamps[(int64_t)(wave_id)*16 + (k)] = t_;  \
+    } while (0)
+#else
+#define GSM_STAMP(p, wave_id, k) do { } while (0)
+#define GSM_RSTAMP(p, wave_id, k) do { } while (0)
+#endif
+
+// number of set bits of `mask` below this lane
+__device__ __forceinline__ int lanes_below(uint64_t mask) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// compact collider index (agents [0,N), obstacles [N,M)) -> entity index
+__device__ __forceinline__ int collider_entity(int c, int N) { return c < N ? c : N + c; }
+
+__device__ __forceinline__ float2 layout_pos(const DevParams &p, uint32_t gid, uint32_t ep,
+                                             uint32_t e) {
+    const Philox4 x = philox4x32_10(e, ep, gid, kTagLayout, p.seed_lo, p.seed_hi);
+    return make_float2(u01(x.x0) * p.twoL - p.L, u01(x.x1) * p.twoL - p.L);
+}
+
+// Environment._set_action + apply_action_force (App. A S5).
+__device__ __forceinline__ float2 action_force(const DevParams &p, int64_t a) {
+    float ux, uy;
+    if (p.action_fmt == 0) {
+        const float *q = (const float *)p.actions + a * 5;
+        ux = q[1] - q[2];
+        uy = q[3] - q[4];
+    } else if (p.action_fmt == 1) {
+        const int k = ((const int32_t *)p.actions)[a];
+        ux = (float)(k == 1) - (float)(k == 2);
+        uy = (float)(k == 3) - (float)(k == 4);
+    } else {
+        const float2 q = ((const float2 *)p.actions)[a];
+        ux = q.x;
+        uy = q.y;
+    }
+    return make_float2(ux * p.sens, uy * p.sens);
+}
+
+// MPE get_collision_force magnitude / d for one pair inside the cutoff:
+//   F/d = c * k * softplus(-(d - dmin)/k) / d.
+// Written as pen = max(D, 0) + k*log1p(exp(-|D|/k)), D = dmin - d: the
+// dominant term max(D, 0) is exact and the transcendental part is a
+// correction < k*ln2, so the hardware v_exp/v_log/v_rcp/v_sqrt (<= 1 ulp)
+// keep |F| within ~2e-7 relative (positions/velocities stay within the 1e-6
+// parity bar).
+__device__ __forceinline__ float contact_scale(const DevParams &p, float d2, float dmin) {
+    const float d = __builtin_amdgcn_sqrtf(d2);
+    const float D = dmin - d;
+    const float e = __expf(-fabsf(D) * p.inv_k);                 // in (0, 1]
+    const float pen = fmaxf(D, 0.0f) + p.k * __logf(1.0f + e);
+    return p.cf * pen * __builtin_amdgcn_rcpf(d);
+}
+
+}  // namespace gsm

@@ -21,74 +21,9 @@
 // counts, edge predicates) is done in fp32 without contraction (the library is
 // built with -ffp-contract=off) in the same order as oracle/batch_ref.py's fp32
 // mode: d2 = dx*dx + dy*dy, collide iff d2 < dmin*dmin, edge iff 0 < d2 <= R*R.
-#include "gsm_internal.h"
-#include "gsm_philox.h"
+#include "gsm_device.h"
 
 namespace gsm {
-
-enum { kModeStep = 0, kModeReset = 1, kModeObserve = 2 };
-
-// Orders LDS traffic between the lanes of one wave: LDS ops of a wave execute
-// in order, so only compiler motion has to be fenced.
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
-__device__ __forceinline__ int wave_sum(int v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-    return v;
-}
-
-// number of set bits of `mask` below this lane
-__device__ __forceinline__ int lanes_below(uint64_t mask) {
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32),
-                                          __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
-}
-
-// compact collider index (agents [0,N), obstacles [N,M)) -> entity index
-__device__ __forceinline__ int collider_entity(int c, int N) { return c < N ? c : N + c; }
-
-__device__ __forceinline__ float2 layout_pos(const DevParams &p, uint32_t gid, uint32_t ep,
-                                             uint32_t e) {
-    const Philox4 x = philox4x32_10(e, ep, gid, kTagLayout, p.seed_lo, p.seed_hi);
-    return make_float2(u01(x.x0) * p.twoL - p.L, u01(x.x1) * p.twoL - p.L);
-}
-
-// Environment._set_action + apply_action_force (App. A S5).
-__device__ __forceinline__ float2 action_force(const DevParams &p, int64_t a) {
-    float ux, uy;
-    if (p.action_fmt == 0) {
-        const float *q = (const float *)p.actions + a * 5;
-        ux = q[1] - q[2];
-        uy = q[3] - q[4];
-    } else if (p.action_fmt == 1) {
-        const int k = ((const int32_t *)p.actions)[a];
-        ux = (float)(k == 1) - (float)(k == 2);
-        uy = (float)(k == 3) - (float)(k == 4);
-    } else {
-        const float2 q = ((const float2 *)p.actions)[a];
-        ux = q.x;
-        uy = q.y;
-    }
-    return make_float2(ux * p.sens, uy * p.sens);
-}
-
-// MPE get_collision_force magnitude / d for one pair with d2 inside the
-// cutoff: c * k * softplus(-(d - dmin)/k) / d (stable logaddexp(0, z)).
-__device__ __forceinline__ float contact_scale(const DevParams &p, float d2, float dmin) {
-    const float d = sqrtf(d2);
-    const float z = -(d - dmin) / p.k;
-    const float sp = fmaxf(z, 0.0f) + log1pf(expf(-fabsf(z)));
-    return p.cf / d * (sp * p.k);
-}
 
 // ---------------------------------------------------------------------------
 // step kernel
@@ -376,7 +311,7 @@ __device__ void env_emit(const DevParams &p, const int b, const int lane, int64_
 __global__ __launch_bounds__(kBlock) void gsm_emit_edges_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    int64_t *s_red = (int64_t *)(smem + kWavesPerBlock * p.wave_lds_emit);
+    int *s_red = (int *)(smem + kWavesPerBlock * p.wave_lds_emit);
     // exclusive prefix of the step kernel's per-workgroup edge sums
     // (host guarantees edge_capacity < 2^31, so int32 sums cannot overflow)
     int acc = 0;
@@ -397,22 +332,32 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_edges_kernel(DevParams p) {
     env_emit(p, b, lane, off, smem + wave * p.wave_lds_emit);
 }
 
-int grid_blocks(const DevParams &p) { return (p.B + kWavesPerBlock - 1) / kWavesPerBlock; }
-const void *step_kernel_fn() { return reinterpret_cast<const void *>(&gsm_step_kernel); }
-const void *emit_kernel_fn() { return reinterpret_cast<const void *>(&gsm_emit_edges_kernel); }
+int grid_blocks(const DevParams &p) {
+    const int per_block = kWavesPerBlock * p.G;
+    return (p.B + per_block - 1) / per_block;
+}
+const void *step_kernel_fn(const DevParams &p) {
+    return p.path == kPathSeg ? step_seg_kernel_fn(p) : reinterpret_cast<const void *>(&gsm_step_kernel);
+}
+const void *emit_kernel_fn(const DevParams &p) {
+    return p.path == kPathSeg ? emit_seg_kernel_fn(p) : reinterpret_cast<const void *>(&gsm_emit_edges_kernel);
+}
 size_t step_kernel_lds(const DevParams &p) { return (size_t)kWavesPerBlock * p.wave_lds_step + 16; }
-size_t emit_kernel_lds(const DevParams &p) { return (size_t)kWavesPerBlock * p.wave_lds_emit + 8 * kWavesPerBlock; }
+size_t emit_kernel_lds(const DevParams &p) { return (size_t)kWavesPerBlock * p.wave_lds_emit + 16; }
+
+static hipError_t launch_fn(const void *fn, const DevParams &p, size_t lds, hipStream_t s) {
+    (void)hipGetLastError();   // report this launch's error only
+    void *args[] = {const_cast<DevParams *>(&p)};
+    const hipError_t e = hipLaunchKernel(fn, dim3(grid_blocks(p)), dim3(kBlock), args, lds, s);
+    return e != hipSuccess ? e : hipGetLastError();
+}
 
 hipError_t launch_step_kernel(const DevParams &p, hipStream_t s) {
-    (void)hipGetLastError();   // report this launch's error only
-    hipLaunchKernelGGL(gsm_step_kernel, dim3(grid_blocks(p)), dim3(kBlock), step_kernel_lds(p), s, p);
-    return hipGetLastError();
+    return launch_fn(step_kernel_fn(p), p, step_kernel_lds(p), s);
 }
 
 hipError_t launch_emit_kernel(const DevParams &p, hipStream_t s) {
-    (void)hipGetLastError();
-    hipLaunchKernelGGL(gsm_emit_edges_kernel, dim3(grid_blocks(p)), dim3(kBlock), emit_kernel_lds(p), s, p);
-    return hipGetLastError();
+    return launch_fn(emit_kernel_fn(p), p, emit_kernel_lds(p), s);
 }
 
 hipError_t launch_step(const DevParams &p, hipStream_t s) {

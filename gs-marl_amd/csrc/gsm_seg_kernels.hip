@@ -1,0 +1,671 @@
+// gsm_seg_kernels.hip — segmented kernels for envs with M = N + No <= 64
+// colliders: the headline 24-agent navigation path and every BASELINE config
+// except the 96-agent one.
+//
+// Lane layout. A wave holds G = min(64 / M, 16) envs ("segments" of M
+// lanes); lane (seg, m) owns row m of its env in compact collider order
+// (m < N: agent m = entity m; m >= N: obstacle m-N = entity N+m). The G envs'
+// positions live in LDS.
+//
+// Observation pass (post-physics positions). The radius adjacency is
+// symmetric, so a wave-uniform sweep over the N *agent* columns j suffices:
+//   * the ballot over lanes of  rad(m, j) = 0 < d2 <= R2  is agent row j's
+//     full mask; lane j captures its segment's slice (v_writelane when G = 1);
+//   * obstacle rows set their agent bits per lane; their obstacle-obstacle
+//     bits are static within an episode and are carried in the stored row
+//     masks (a reset or an observe recomputes them with a full sweep);
+//   * the ballot of  d2 < dmin2  gives agent j's collision count (popcount),
+//   * the ballot of  0 < d2 < (dmin + cutoff)^2  gives agent j's contact
+//     candidates, stored for the NEXT step's force pass (same positions).
+// All predicates use d2 = dx*dx + dy*dy without FMA (bit-exact contract).
+//
+// Physics pass (pre-step positions): agent lane i sums the contact force of
+// its stored candidates only (ascending collider index), then integrates.
+//
+// Emission (gsm_emit_seg_kernel): row masks -> per-row counts in entity order
+// (agent rows, goal rows, obstacle rows) -> lane scan -> each lane writes its
+// row (agent columns, own goal, obstacle columns); agent lanes also write the
+// goal rows. CSR offsets come from the per-workgroup sums of the step kernel:
+// no atomics, no inter-workgroup waiting, deterministic.
+//
+// With one env per wave (G = 1, e.g. 24 agents) the segment collectives are
+// DPP wave scans/reductions and per-env scalars are scalar loads.
+#include <type_traits>
+
+#include "gsm_device.h"
+
+namespace gsm {
+
+template <typename T>
+__device__ __forceinline__ T seg_scan(T v, int m) {   // inclusive scan within a segment
+#pragma unroll
+    for (int o = 1; o < kWave; o <<= 1) {
+        const T u = __shfl_up(v, o);
+        if (m >= o) v += u;
+    }
+    return v;
+}
+
+__device__ __forceinline__ int row_entity(int m, int N) { return m < N ? m : N + m; }
+
+template <int kN, int kNo>
+constexpr int envs_per_wave() {
+    return kN > 0 ? ((kWave / (kN + kNo)) > kMaxSegEnvsPerWave ? kMaxSegEnvsPerWave : kWave / (kN + kNo))
+                  : 0;
+}
+
+// compile-time shape when kN > 0, runtime otherwise
+template <int kN, int kNo>
+struct Shape {
+    int N, No, M, E, G;
+    __device__ __forceinline__ explicit Shape(const DevParams &p) {
+        if constexpr (kN > 0) {
+            N = kN;
+            No = kNo;
+            M = kN + kNo;
+            E = 2 * kN + kNo;
+            G = envs_per_wave<kN, kNo>();
+        } else {
+            N = p.N;
+            No = p.No;
+            M = p.N + p.No;
+            E = p.E;
+            G = p.G;
+        }
+    }
+};
+
+struct Lane {
+    int lane, seg, m, b, base, wave;    // base = first lane of the segment
+    bool live, agent;
+};
+
+template <int kN, int kNo>
+__device__ __forceinline__ Lane seg_lane(const DevParams &p, const Shape<kN, kNo> &s) {
+    Lane L;
+    L.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    L.lane = threadIdx.x & 63;
+    if constexpr (envs_per_wave<kN, kNo>() == 1) {
+        L.seg = 0;
+        L.base = 0;
+        L.m = L.lane;
+        L.b = blockIdx.x * kWavesPerBlock + L.wave;          // wave-uniform
+        L.live = L.lane < s.M && L.b < p.B;
+    } else {
+        L.seg = L.lane / s.M;
+        L.base = L.seg * s.M;
+        L.m = L.lane - L.base;
+        L.b = (blockIdx.x * kWavesPerBlock + L.wave) * s.G + L.seg;
+        L.live = L.seg < s.G && L.b < p.B;
+    }
+    L.agent = L.live && L.m < s.N;
+    return L;
+}
+
+// a wave-uniform 64-bit ballot restricted to this lane's segment, delivered
+// to the lane whose row index is j (other lanes keep `old`)
+template <int kG>
+__device__ __forceinline__ uint64_t capture(uint64_t ballot, int j, const Lane &L, uint64_t segmask,
+                                            uint64_t old) {
+    if constexpr (kG == 1) {
+        const uint64_t v = ballot & segmask;
+        const uint32_t lo = writelane_u32((uint32_t)v, (uint32_t)j, (uint32_t)old);
+        const uint32_t hi = writelane_u32((uint32_t)(v >> 32), (uint32_t)j, (uint32_t)(old >> 32));
+        return ((uint64_t)hi << 32) | lo;
+    } else {
+        const uint64_t mine = (ballot >> L.base) & segmask;
+        return L.m == j ? mine : old;
+    }
+}
+template <int kG>
+__device__ __forceinline__ int capture_count(uint64_t ballot, int j, const Lane &L, uint64_t segmask,
+                                             int old) {
+    if constexpr (kG == 1) {
+        return (int)writelane_u32((uint32_t)__popcll(ballot & segmask), (uint32_t)j, (uint32_t)old);
+    } else {
+        const int mine = __popcll((ballot >> L.base) & segmask);
+        return L.m == j ? mine : old;
+    }
+}
+
+// sum over the lanes of this lane's segment (every lane of the segment gets it)
+template <int kG, typename T>
+__device__ __forceinline__ T seg_total(T v, const Lane &L, int M) {
+    if constexpr (kG == 1) {
+        return wave_total(v);
+    } else {
+        return __shfl(seg_scan(v, L.m), L.base + M - 1);
+    }
+}
+
+// agent-column bits of one row: 32 bits suffice when N <= 32 is known
+template <int kN>
+using OwnBits = typename std::conditional<(kN > 0 && kN <= 32), uint32_t, uint64_t>::type;
+
+// Observation sweep (file header). row/cand/ccnt are per lane: row = radius
+// row mask (compact bits), cand = contact candidates (agent lanes),
+// ccnt = collisions of agent lanes (self excluded). With full = false the
+// obstacle-obstacle bits are taken from `oo` (the cached masks).
+template <int kN, int kNo, int kG>
+__device__ __forceinline__ void obs_sweep(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L,
+                                          const float2 *sp, float2 pm, bool full, uint64_t oo,
+                                          uint64_t &row, uint64_t &cand, int &ccnt) {
+    const int N = s.N, M = s.M;
+    const uint64_t segmask = M >= 64 ? ~0ull : ((1ull << M) - 1);
+    const uint64_t abits = N >= 64 ? ~0ull : ((1ull << N) - 1);
+    const bool obst = L.m >= N;
+    (void)abits;
+    const float dmin2 = obst ? p.dmin2_ao : p.dmin2_aa;   // lane m vs an agent column
+    // For a non-negative float d2 the bit pattern is monotone, so with
+    // t = bits(d2) - 1 (d2 = +0 wraps to 0xffffffff):
+    //   0 < d2 <= R2    <=>  t <u bits(R2)
+    //   0 < d2 < cut2   <=>  t <u bits(cut2) - 1      (same predicates, one compare each)
+    const uint32_t r2b = __float_as_uint(p.R2);
+    const uint32_t cutb = __float_as_uint(obst ? p.cut2_ao : p.cut2_aa) - 1u;
+    uint64_t r = (!full && obst) ? (oo & segmask & ~abits) : 0ull;
+    uint64_t c = 0;
+    OwnBits<kN> own = 0;                                    // per-lane agent bits (obstacle rows)
+    int cc = 0;
+#pragma unroll 4
+    for (int j = 0; j < N; ++j) {
+        const float2 q = sp[j];
+        const float dx = pm.x - q.x, dy = pm.y - q.y;
+        const float d2 = dx * dx + dy * dy;
+        const uint32_t t = __float_as_uint(d2) - 1u;
+        const bool rad = t < r2b;
+        const uint64_t b_rad = __ballot(rad);
+        const uint64_t b_cand = __ballot(t < cutb);
+        const uint64_t b_col = __ballot(d2 < dmin2);
+        own |= (OwnBits<kN>)rad << j;
+        r = capture<kG>(b_rad, j, L, segmask, r);
+        c = capture<kG>(b_cand, j, L, segmask, c);
+        cc = capture_count<kG>(b_col, j, L, segmask, cc);
+    }
+    if (obst) r |= own;                                     // agent bits of obstacle rows
+    if (full) {
+        // obstacle columns: obstacle-obstacle bits (the agent-obstacle bits
+        // of agent rows were captured above)
+        for (int k = N; k < M; ++k) {
+            const float2 q = sp[N + k];
+            const float dx = pm.x - q.x, dy = pm.y - q.y;
+            const float d2 = dx * dx + dy * dy;
+            if (obst && d2 > 0.0f && d2 <= p.R2) r |= 1ull << k;
+        }
+    }
+    row = r;
+    cand = c;
+    ccnt = cc - 1;                                          // the self pair (d2 = 0 < dmin2)
+}
+
+// Environment._set_action for a compile-time action format (kFmt < 0: runtime)
+template <int kFmt>
+__device__ __forceinline__ float2 action_force_t(const DevParams &p, int64_t a) {
+    if constexpr (kFmt < 0) {
+        return action_force(p, a);
+    } else {
+        float ux, uy;
+        if constexpr (kFmt == 0) {
+            const float *q = (const float *)p.actions + a * 5;
+            ux = q[1] - q[2];
+            uy = q[3] - q[4];
+        } else if constexpr (kFmt == 1) {
+            const int k = ((const int32_t *)p.actions)[a];
+            ux = (float)(k == 1) - (float)(k == 2);
+            uy = (float)(k == 3) - (float)(k == 4);
+        } else {
+            const float2 q = ((const float2 *)p.actions)[a];
+            ux = q.x;
+            uy = q.y;
+        }
+        return make_float2(ux * p.sens, uy * p.sens);
+    }
+}
+
+// node-feature row of entity e: vx vy px py gx-px gy-py type
+__device__ __forceinline__ void store_row(float *nf, float2 v, float2 pos, float2 grel, float type) {
+    nf[0] = v.x;
+    nf[1] = v.y;
+    nf[2] = pos.x;
+    nf[3] = pos.y;
+    nf[4] = grel.x;
+    nf[5] = grel.y;
+    nf[6] = type;
+}
+
+// ---------------------------------------------------------------------------
+#ifdef GSM_STEP_SGPR   // experiment: SGPR budget (residency = floor(800 / (ceil(sgpr/16)*16 + 16)) waves/SIMD)
+#define GSM_STEP_ATTR __attribute__((amdgpu_num_sgpr(GSM_STEP_SGPR)))
+#else
+#define GSM_STEP_ATTR
+#endif
+template <int kN, int kNo, int kFmt>
+__global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const Shape<kN, kNo> s(p);
+    constexpr int kG = envs_per_wave<kN, kNo>();
+    const Lane L = seg_lane(p, s);
+    const int N = s.N, E = s.E, M = s.M, G = s.G;
+    const int wave = L.wave;
+    const int segc = L.seg < G ? L.seg : G - 1;             // clamp idle lanes' addresses
+    float2 *s_pos = (float2 *)(smem + wave * p.wave_lds_step) + segc * E;
+    float *s_nf = (float *)((float2 *)(smem + wave * p.wave_lds_step) + G * E);   // [G][E][7]
+    const int m = L.m;
+    const bool obst = L.live && m >= N;
+    const bool wave_live = kG == 1 ? L.b < p.B : true;
+    // per-env base pointers: wave-uniform (scalar) when G = 1; lane offsets
+    // below are 32-bit
+    const int64_t eb = kG == 1 ? (wave_live ? L.b : 0) : (L.live ? L.b : 0);
+    float2 *const pos_b = p.pos + eb * E;
+    float2 *const vel_b = p.vel + eb * N;
+    const uint32_t um = (uint32_t)m;
+    const int64_t wid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+    GSM_RSTAMP(p, wid, 8);
+    GSM_STAMP(p, wid, 0);
+
+    // ---- load: issue every global load before the first wait
+    int t = 0, ep = 0;
+    float2 acc = make_float2(0.0f, 0.0f);
+    float2 v = make_float2(0.0f, 0.0f), u = make_float2(0.0f, 0.0f);
+    uint64_t cand_prev = 0, oo = 0;
+    if constexpr (kG == 1) {
+        if (wave_live) {
+            float2 x0 = make_float2(0.0f, 0.0f), x1 = x0;
+            if (L.lane < E) x0 = pos_b[(uint32_t)L.lane];
+            if (L.lane + kWave < E) x1 = pos_b[(uint32_t)(L.lane + kWave)];
+            t = p.step_count[L.b];
+            ep = p.episode[L.b];
+            acc = p.ep_acc[L.b];
+            if (L.agent) {
+                v = vel_b[um];
+                if (p.mode == kModeStep) {
+                    u = action_force_t<kFmt>(p, eb * N + um);
+                    cand_prev = (p.contact_mask + eb * N)[um];
+                }
+            }
+            if (obst && p.mode == kModeStep) oo = (p.row_mask + eb * M)[um];
+            if (L.lane < E) s_pos[L.lane] = x0;
+            if (L.lane + kWave < E) s_pos[L.lane + kWave] = x1;
+        }
+    } else {
+        if (L.live) {
+            for (int e = m; e < E; e += M) s_pos[e] = p.pos[eb * E + e];
+            t = p.step_count[L.b];
+            ep = p.episode[L.b];
+            acc = p.ep_acc[L.b];
+        }
+        if (L.agent) {
+            v = p.vel[eb * N + m];
+            if (p.mode == kModeStep) {
+                u = action_force_t<kFmt>(p, eb * N + m);
+                cand_prev = p.contact_mask[eb * N + m];
+            }
+        }
+        if (obst && p.mode == kModeStep) oo = p.row_mask[eb * M + m];
+    }
+    bool reset = L.live && p.mode == kModeReset && (p.env_mask == nullptr || p.env_mask[L.b] != 0);
+    wave_sync();
+    GSM_STAMP(p, wid, 1);
+
+    // scenario.reset_world (Philox layout, App. A S14) for the lanes' envs
+    auto relayout = [&]() {
+        if (reset) {
+            ep = (p.mode == kModeReset && p.reseed ? -1 : ep) + 1;
+            t = 0;
+            acc = make_float2(0.0f, 0.0f);
+            v = make_float2(0.0f, 0.0f);
+            const uint32_t gid = (uint32_t)(p.env_base + L.b);
+            for (int e = m; e < E; e += M) s_pos[e] = layout_pos(p, gid, (uint32_t)ep, (uint32_t)e);
+        }
+        wave_sync();
+    };
+    if (__any(reset)) relayout();
+
+    bool done = false;
+    if (p.mode == kModeStep) {
+        // apply_environment_force over the candidates found on these positions
+        // by the previous observation pass, then integrate_state (App. A S6)
+        if (L.agent) {
+            const float2 pi = s_pos[m];
+            float Fx = u.x, Fy = u.y;
+            uint64_t cm = cand_prev;
+#ifdef GSM_ABL_NO_CONTACT   // timing-only
+            cm = 0;
+#endif
+            while (cm) {
+                const int c = __builtin_ctzll(cm);
+                cm &= cm - 1;
+                const bool ag = c < N;
+                const float2 pj = s_pos[row_entity(c, N)];
+                const float dx = pi.x - pj.x, dy = pi.y - pj.y;
+                const float d2 = dx * dx + dy * dy;
+                const float f = contact_scale(p, d2, ag ? p.dmin_aa : p.dmin_ao);
+                Fx += f * dx;
+                Fy += f * dy;
+            }
+            v.x = v.x * p.omd;
+            v.y = v.y * p.omd;
+            v.x = v.x + (Fx * p.inv_mass) * p.dt;
+            v.y = v.y + (Fy * p.inv_mass) * p.dt;
+            if (p.max_speed > 0.0f) {
+                const float sp = sqrtf(v.x * v.x + v.y * v.y);
+                if (sp > p.max_speed) {
+                    v.x = v.x / sp * p.max_speed;
+                    v.y = v.y / sp * p.max_speed;
+                }
+            }
+            float2 np;
+            np.x = pi.x + v.x * p.dt;
+            np.y = pi.y + v.y * p.dt;
+            s_pos[m] = np;
+        }
+        wave_sync();
+        t += 1;
+        done = L.live && t >= p.EL;
+    }
+
+    GSM_STAMP(p, wid, 2);
+    // ---- observation pass on the post-physics positions
+    const bool full = p.mode != kModeStep;                  // reset / observe: recompute obstacle pairs
+    float2 pm = s_pos[row_entity(m, N)];
+    uint64_t row, cand;
+    int ccnt;
+#ifdef GSM_ABL_NO_SWEEP   // timing-only
+    row = oo; cand = 0; ccnt = 0;
+    asm volatile("" :: "v"(pm.x), "v"(pm.y));
+#else
+    obs_sweep<kN, kNo, kG>(p, s, L, s_pos, pm, full, oo, row, cand, ccnt);
+#endif
+
+    GSM_STAMP(p, wid, 3);
+    // reward / cost callbacks
+    float r = 0.0f;
+    if (L.agent) {
+        const float2 g = s_pos[N + m];
+        const float dx = pm.x - g.x, dy = pm.y - g.y;
+        r = -__builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+    }
+    GSM_STAMP(p, wid, 10);
+    float rsum = seg_total<kG>(r, L, M);
+    const int ci = L.agent ? ccnt : 0;
+    const int csum = seg_total<kG>(ci, L, M);
+    GSM_STAMP(p, wid, 11);
+    if (L.agent) {
+        (p.reward + eb * N)[um] = p.shared_reward ? rsum : r;
+        (p.cost + eb * N)[um] = (float)ci;
+    }
+    GSM_STAMP(p, wid, 12);
+    if (p.shared_reward) rsum *= (float)N;
+    bool relaid = reset;                                    // layout changed in this launch
+    if (p.mode == kModeStep) {
+        if (L.live) {
+            acc.x += rsum;
+            acc.y += (float)csum;
+        }
+        if (done && p.auto_reset) {
+            reset = true;
+            if (m == 0) p.ep_last[L.b] = acc;
+        }
+        if (__any(reset)) {
+            // auto-reset: new layout, then the graph part of the observation again
+            relayout();
+            const float2 pm2 = s_pos[row_entity(m, N)];
+            uint64_t row2, cand2;
+            int cc2;
+            obs_sweep<kN, kNo, kG>(p, s, L, s_pos, pm2, true, 0ull, row2, cand2, cc2);
+            if (reset) {
+                pm = pm2;
+                row = row2;
+                cand = cand2;
+            }
+            relaid = reset;
+        }
+    }
+    if (!L.live) row = 0;
+    GSM_STAMP(p, wid, 4);
+
+    // ---- outputs and state. Node features: agent rows every step; goal and
+    // obstacle rows (static within an episode) only when the layout is new or
+    // on an observe. Rows are staged in LDS and stored lane-linear.
+    const bool any_statics = p.mode != kModeStep || __any(relaid);
+    if (L.live) {
+        float *nf = s_nf + segc * E * 7;
+        if (L.agent) {
+            const float2 g = s_pos[N + m];
+            store_row(nf + m * 7, v, pm, make_float2(g.x - pm.x, g.y - pm.y), 0.0f);
+            if (any_statics)
+                store_row(nf + (N + m) * 7, make_float2(0.0f, 0.0f), g, make_float2(0.0f, 0.0f), 1.0f);
+        } else if (any_statics) {
+            store_row(nf + (N + m) * 7, make_float2(0.0f, 0.0f), pm, make_float2(0.0f, 0.0f), 2.0f);
+        }
+        if (relaid) {
+            for (int e = m; e < E; e += M) pos_b[(uint32_t)e] = s_pos[e];
+        } else if (L.agent && p.mode == kModeStep) {
+            pos_b[um] = pm;
+        }
+        if (L.agent && (p.mode == kModeStep || relaid)) vel_b[um] = v;
+        if (L.agent) (p.contact_mask + eb * N)[um] = cand;
+        (p.row_mask + eb * M)[um] = row;
+    }
+    wave_sync();
+    {
+        const int b0 = kG == 1 ? L.b : (blockIdx.x * kWavesPerBlock + wave) * G;
+        for (int g = 0; g < G; ++g) {
+            if (b0 + g >= p.B) break;
+            // per env, not per lane: idle lanes of the env's wave copy too
+            const bool full_rows = p.mode != kModeStep || (kG == 1 ? __any(relaid) : __shfl(relaid, g * M));
+            const int len = (full_rows ? E : N) * 7;
+            float *dst = p.node_feat + (int64_t)(b0 + g) * E * 7;
+            const float *src = s_nf + g * E * 7;
+#ifdef GSM_ABL_NO_NF   // timing-only
+            if (len > 0) continue;
+#endif
+            for (int q = L.lane; q < len; q += kWave) dst[(uint32_t)q] = src[q];
+        }
+    }
+
+    GSM_STAMP(p, wid, 5);
+    // edge count (radius rows + goal edges both ways)
+    const int edges = __popcll(row) + ((L.live && m == 0) ? 2 * N : 0);
+    int wave_edges;
+    if constexpr (kG == 1) {
+        wave_edges = wave_total(edges);
+        if (wave_live && L.lane == 0) {
+            p.step_count[L.b] = t;
+            p.episode[L.b] = ep;
+            p.ep_acc[L.b] = acc;
+            p.done[L.b] = done ? 1 : 0;
+            p.edge_count[L.b] = wave_edges;
+        }
+    } else {
+        wave_edges = wave_sum(edges);
+        const int env_edges = seg_total<kG>(edges, L, M);
+        if (L.live && m == 0) {
+            p.step_count[L.b] = t;
+            p.episode[L.b] = ep;
+            p.ep_acc[L.b] = acc;
+            p.done[L.b] = done ? 1 : 0;
+            p.edge_count[L.b] = env_edges;
+        }
+    }
+    int *s_bc = (int *)(smem + kWavesPerBlock * p.wave_lds_step);
+    if (L.lane == 0) s_bc[wave] = wave_edges;
+    GSM_STAMP(p, wid, 6);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int q = 0;
+        for (int k = 0; k < kWavesPerBlock; ++k) q += s_bc[k];
+        p.block_edge_sum[blockIdx.x] = q;
+    }
+    GSM_STAMP(p, wid, 7);
+    GSM_RSTAMP(p, wid, 9);
+}
+
+// ---------------------------------------------------------------------------
+template <int kN, int kNo>
+__global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const Shape<kN, kNo> s(p);
+    constexpr int kG = envs_per_wave<kN, kNo>();
+    const Lane L = seg_lane(p, s);
+    const int N = s.N, E = s.E, M = s.M, G = s.G;
+    const int wave = L.wave;
+    const int segc = L.seg < G ? L.seg : G - 1;
+    float2 *s_pos = (float2 *)(smem + wave * p.wave_lds_emit) + segc * E;
+    int *s_red = (int *)(smem + kWavesPerBlock * p.wave_lds_emit);
+    const int m = L.m;
+    const int64_t eb = L.live ? L.b : 0;
+    const int64_t wid = (int64_t)(gridDim.x + blockIdx.x) * kWavesPerBlock + wave;
+    GSM_RSTAMP(p, wid, 8);
+    GSM_STAMP(p, wid, 0);
+
+    // inputs independent of the prefix first
+    uint64_t mask = 0;
+    if constexpr (kG == 1) {
+        if (L.b < p.B) {
+            const float2 *src = p.pos + (int64_t)L.b * E;
+            if (L.lane < E) s_pos[L.lane] = src[L.lane];
+            if (L.lane + kWave < E) s_pos[L.lane + kWave] = src[L.lane + kWave];
+            if (L.live) mask = p.row_mask[eb * M + m];
+        }
+    } else if (L.live) {
+        for (int e = m; e < E; e += M) s_pos[e] = p.pos[eb * E + e];
+        mask = p.row_mask[eb * M + m];
+    }
+    // global offset of this block: prefix of the step kernel's block sums
+    int acc = 0;
+#ifdef GSM_ABL_NO_PREFIX   // timing-only ablation build (wrong offsets)
+    if (false)
+#endif
+    {
+        const int nb = (int)blockIdx.x;
+        const int nb4 = nb & ~3;
+        const int4 *bs4 = (const int4 *)p.block_edge_sum;
+        for (int k = threadIdx.x; 4 * k < nb4; k += kBlock) {
+            const int4 q = bs4[k];
+            acc += q.x + q.y + q.z + q.w;
+        }
+        if ((int)threadIdx.x < nb - nb4) acc += p.block_edge_sum[nb4 + threadIdx.x];
+    }
+    acc = wave_total(acc);
+    GSM_STAMP(p, wid, 1);
+    if (L.lane == 0) s_red[wave] = acc;
+    // envs of this block in order before this lane's env
+    int64_t env_off;
+    int my_cnt;
+    if constexpr (kG == 1) {
+        const int first = blockIdx.x * kWavesPerBlock;
+        int before = 0;
+        for (int q = 0; q < wave; ++q) before += p.edge_count[first + q];
+        my_cnt = L.b < p.B ? p.edge_count[L.b] : 0;
+        __syncthreads();
+        int64_t base = 0;
+        for (int q = 0; q < kWavesPerBlock; ++q) base += s_red[q];
+        env_off = base + before;
+    } else {
+        const int first = blockIdx.x * kWavesPerBlock * G;
+        const int nblk = min(kWavesPerBlock * G, p.B - first);
+        const int cnt_k = L.lane < nblk ? p.edge_count[first + L.lane] : 0;
+        const int incl_k = wave_scan(cnt_k);
+        __syncthreads();
+        int64_t base = 0;
+        for (int q = 0; q < kWavesPerBlock; ++q) base += s_red[q];
+        const int kk = L.live ? L.b - first : 0;
+        my_cnt = __shfl(cnt_k, kk);
+        env_off = base + __shfl(incl_k, kk) - my_cnt;
+    }
+    if (L.live && m == 0) {
+        p.edge_ptr[L.b] = env_off;
+        if (L.b == p.B - 1) p.edge_ptr[p.B] = env_off + my_cnt;
+    }
+    GSM_STAMP(p, wid, 2);
+
+    // row offsets in entity order: agent rows, goal rows, obstacle rows
+    const int c = __popcll(mask) + (L.agent ? 1 : 0);
+    int incl, a_total;
+    if constexpr (kG == 1) {
+        incl = wave_scan(c);
+        a_total = __builtin_amdgcn_readlane(incl, N - 1);
+    } else {
+        incl = seg_scan(c, m);
+        a_total = __shfl(incl, L.base + N - 1);
+    }
+    int64_t o = env_off + incl - c + (m >= N ? N : 0);
+    GSM_STAMP(p, wid, 3);
+    if (!L.live) return;
+#ifdef GSM_ABL_NO_EMIT_STORES   // timing-only: every edge store hits one slot
+    o = 0;
+    env_off = 0;
+#endif
+
+    const float2 pm = s_pos[row_entity(m, N)];
+    int32_t *src = p.edge_index, *dst = p.edge_index + p.edge_capacity;
+    float *attr = p.edge_attr;
+    const int32_t g0 = (int32_t)(eb * E);
+    const int32_t gs = g0 + row_entity(m, N);
+    const uint64_t agent_bits = N >= 64 ? ~0ull : ((1ull << N) - 1);
+    uint64_t lo = mask & agent_bits, hi = mask & ~agent_bits;
+    while (lo) {
+        const int j = __builtin_ctzll(lo);
+        lo &= lo - 1;
+        const float2 q = s_pos[j];
+        const float dx = pm.x - q.x, dy = pm.y - q.y;
+        src[o] = gs;
+        dst[o] = g0 + j;
+        attr[o] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+        ++o;
+    }
+    if (L.agent) {
+        const float2 g = s_pos[N + m];
+        const float dx = pm.x - g.x, dy = pm.y - g.y;
+        const float d = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+        src[o] = gs;                    // agent m -> its goal
+        dst[o] = g0 + N + m;
+        attr[o] = d;
+        ++o;
+        const int64_t og = env_off + a_total + m;
+        src[og] = g0 + N + m;           // goal row: goal m -> agent m
+        dst[og] = gs;
+        attr[og] = d;
+    }
+    while (hi) {
+        const int j = __builtin_ctzll(hi);
+        hi &= hi - 1;
+        const float2 q = s_pos[N + j];
+        const float dx = pm.x - q.x, dy = pm.y - q.y;
+        src[o] = gs;
+        dst[o] = g0 + N + j;
+        attr[o] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+        ++o;
+    }
+    GSM_STAMP(p, wid, 4);
+    GSM_RSTAMP(p, wid, 9);
+}
+
+// Specialisations with compile-time shapes (segment arithmetic folded, G = 1
+// collectives for 24 agents) and action formats; anything else runs the
+// runtime-shape instantiation.
+#define GSM_SEG_SHAPES(X) X(3, 3) X(24, 24)
+
+const void *step_seg_kernel_fn(const DevParams &p) {
+#define GSM_PICK(n, no)                                                                       \
+    if (p.N == n && p.No == no) {                                                             \
+        switch (p.action_fmt) {                                                               \
+            case 0: return reinterpret_cast<const void *>(&gsm_step_seg_kernel<n, no, 0>);    \
+            case 1: return reinterpret_cast<const void *>(&gsm_step_seg_kernel<n, no, 1>);    \
+            default: return reinterpret_cast<const void *>(&gsm_step_seg_kernel<n, no, 2>);   \
+        }                                                                                     \
+    }
+    GSM_SEG_SHAPES(GSM_PICK)
+#undef GSM_PICK
+    return reinterpret_cast<const void *>(&gsm_step_seg_kernel<0, 0, -1>);
+}
+
+const void *emit_seg_kernel_fn(const DevParams &p) {
+#define GSM_PICK(n, no) \
+    if (p.N == n && p.No == no) return reinterpret_cast<const void *>(&gsm_emit_seg_kernel<n, no>);
+    GSM_SEG_SHAPES(GSM_PICK)
+#undef GSM_PICK
+    return reinterpret_cast<const void *>(&gsm_emit_seg_kernel<0, 0>);
+}
+
+}  // namespace gsm

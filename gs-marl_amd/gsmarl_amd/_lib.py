@@ -10,8 +10,8 @@ import ctypes as C
 import os
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "lib" / "libgsm.so"
-ABI_VERSION = 1
+LIB_PATH = Path(os.environ.get("GSM_LIB_PATH") or Path(__file__).resolve().parent / "lib" / "libgsm.so")
+ABI_VERSION = 2
 
 GSM_OK, GSM_EINVAL, GSM_EHIP, GSM_ESTATE = 0, -1, -2, -3
 GRAPH_SLOTS = 4
@@ -42,7 +42,7 @@ class GsmSizes(C.Structure):
 
 BUFFER_FIELDS = ["pos", "vel", "step_count", "episode", "ep_acc", "ep_last", "node_feat",
                  "reward", "cost", "done", "edge_count", "block_edge_sum", "edge_ptr",
-                 "edge_index", "edge_attr"]
+                 "edge_index", "edge_attr", "row_mask", "contact_mask"]
 
 
 class GsmBuffers(C.Structure):
@@ -62,6 +62,7 @@ SIGNATURES = {
     "gsm_graph_capture": (C.c_int, [_P, C.c_int32, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int, C.c_int]),
     "gsm_graph_launch": (C.c_int, [_P, C.c_int32, _P]),
     "gsm_graph_kernel_ms": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    "gsm_debug_set_stamps": (C.c_int, [_P, _P]),
     "gsm_destroy": (C.c_int, [_P]),
     "gsm_last_error": (C.c_int, [_P, C.c_char_p, C.c_size_t]),
 }

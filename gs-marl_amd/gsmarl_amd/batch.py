@@ -66,6 +66,9 @@ class GpuBatchEnv:
             edge_ptr=torch.zeros(B + 1, dtype=torch.int64, device=dev),
             edge_index=torch.zeros(2, cap, dtype=i32, device=dev),
             edge_attr=torch.zeros(cap, dtype=f32, device=dev),
+            # derived state (refreshed by every reset/step/observe)
+            row_mask=torch.zeros(B, N + cfg.n_obstacles, dtype=torch.int64, device=dev),
+            contact_mask=torch.zeros(B, N, dtype=torch.int64, device=dev),
         )
         bufs = _lib.GsmBuffers(**{k: self.t[k].data_ptr() for k in _lib.BUFFER_FIELDS})
         _lib.check(self.lib, self.lib.gsm_bind(self._h, C.byref(bufs)), self._h, "gsm_bind")
@@ -154,12 +157,14 @@ class GpuBatchEnv:
     def get_state(self) -> dict:
         return {k: self.t[k].clone() for k in self.STATE_KEYS}
 
-    def set_state(self, state: dict, observe: bool = True) -> Optional[dict]:
+    def set_state(self, state: dict, sync_edges: bool = True) -> dict:
+        """Overwrite state buffers and re-observe (which also refreshes the
+        derived per-position state the next step relies on)."""
         for k, v in state.items():
             if k not in self.STATE_KEYS:
                 raise KeyError(k)
             self.t[k].copy_(torch.as_tensor(v).to(self.t[k].dtype))
-        return self.observe() if observe else None
+        return self.observe(sync_edges)
 
     # ------------------------------------------------------------ HIP graph
     def capture(self, actions_seq: torch.Tensor, n_steps: int, timing: bool = False, slot: int = 0) -> None:

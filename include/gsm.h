@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GSM_ABI_VERSION 1
+#define GSM_ABI_VERSION 2
 
 typedef enum gsm_status {
     GSM_OK = 0,
@@ -110,6 +110,10 @@ typedef struct gsm_buffers {
     int64_t *edge_ptr;        /* [B+1]       CSR offsets into edge arrays     */
     int32_t *edge_index;      /* [2][edge_capacity] global node ids (b*E+e)   */
     float *edge_attr;         /* [edge_capacity]    distance                  */
+    /* derived state, valid for the positions in `pos` after any reset/step/
+     * observe; a caller that rewrites `pos`/`vel` must call gsm_observe      */
+    uint64_t *row_mask;       /* [B][N+No] radius adjacency rows (bit = collider) */
+    uint64_t *contact_mask;   /* [B][N]    contact candidates of each agent        */
 } gsm_buffers;
 
 typedef struct gsm_handle gsm_handle;
@@ -153,6 +157,11 @@ int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream);
 /* After a timed launch of `slot` has completed: mean duration (ms) of the
  * step kernel and of the edge-emit kernel over the captured steps. */
 int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_mean_ms, float *emit_mean_ms);
+
+/* Diagnostics: device buffer (uint64 [2 * n_blocks * 4][16]) that libraries
+ * built with -DGSM_STAMPS fill with per-wave phase timestamps; ignored by the
+ * product build. NULL disables. */
+int gsm_debug_set_stamps(gsm_handle *h, void *stamps);
 
 int gsm_destroy(gsm_handle *h);
 

@@ -108,7 +108,7 @@ def _inject_random(env, ocfg, L, seed, vel_scale=1.0):
     return pos, vel
 
 
-@pytest.mark.parametrize("N,No,B,L", [(3, 3, 64, 0.35), (24, 24, 256, 1.2), (24, 24, 256, 2.83),
+@pytest.mark.parametrize("N,No,B,L", [(3, 3, 64, 0.35), (24, 24, 256, 1.2), (24, 24, 256, 2.83), (5, 2, 37, 0.5), (32, 32, 9, 1.6), (24, 24, 8, 0.3), (8, 8, 16, 0.2),
                                       (96, 96, 16, 3.0), (64, 0, 8, 1.0), (65, 7, 8, 1.5), (1, 0, 4, 1.0)])
 def test_one_step_physics_parity(N, No, B, L):
     env, ocfg = _env(n_agents=N, n_obstacles=No, n_envs=B, episode_length=1000)
@@ -178,7 +178,7 @@ def test_boundary_predicates_exact():
     assert _np(out["cost"]).tolist() == [[1.0, 1.0]]
     # coincident agents: guarded force, counted collision, no radius edge
     pos[0, 1] = pos[0, 0]
-    env.set_state(dict(pos=torch.from_numpy(pos), vel=torch.zeros(1, 2, 2)), observe=False)
+    env.set_state(dict(pos=torch.from_numpy(pos), vel=torch.zeros(1, 2, 2)))
     out = env.step(torch.zeros(1, 2, dtype=torch.int32, device=DEV))
     assert np.all(np.isfinite(_np(env.t["pos"])))
     check_outputs(env, ocfg, out)

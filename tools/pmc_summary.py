@@ -1,0 +1,36 @@
+"""Summarise rocprofv3 --pmc CSVs (tools/pmc.sh) per kernel: mean counter
+value per dispatch, plus derived per-wave instruction counts and HBM bytes
+(FETCH_SIZE x2 on gfx950 per MI355X_MICROARCH.md §HBM; both in KiB)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+root = sys.argv[1]
+acc = defaultdict(lambda: defaultdict(list))
+for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), recursive=True):
+    with open(f) as fh:
+        for row in csv.DictReader(fh):
+            name = row.get("Kernel_Name", "")
+            if "gsm" not in name:
+                continue
+            short = "step" if "step" in name else ("emit" if "emit" in name else name[:40])
+            acc[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
+out = {}
+for k, d in acc.items():
+    m = {c: sum(v) / len(v) for c, v in d.items()}
+    waves = m.get("SQ_WAVES", 0) or 1
+    der = {}
+    for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR"):
+        if c in m:
+            der[c + "_per_wave"] = m[c] / waves
+    if "SQ_WAVE_CYCLES" in m:
+        der["wave_cycles_per_wave(x4)"] = m["SQ_WAVE_CYCLES"] / waves
+    if "FETCH_SIZE" in m:
+        der["hbm_read_bytes_corrected"] = 2 * m["FETCH_SIZE"] * 1024
+    if "WRITE_SIZE" in m:
+        der["hbm_write_bytes"] = m["WRITE_SIZE"] * 1024
+    out[k] = dict(counters=m, derived=der, dispatches=len(next(iter(d.values()))))
+print(json.dumps(out, indent=1))
