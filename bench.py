@@ -38,19 +38,44 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def step_kernel_bytes(B, N, No, EL, action_bytes):
-    """Algorithmic HBM bytes of one gsm_step_kernel launch."""
-    E = 2 * N + No
-    reads = 8 * E + 8 * N + action_bytes * N + 16
-    writes = 8 * N + 8 * N + 28 * E + 4 * N + 4 * N + 1 + 4 + 16 + 1
-    reset = ((E - N) * 8 + 8) / EL          # amortised re-layout write
-    return B * (reads + writes + reset)
+def step_kernel_bytes(B, N, No, EL, action_bytes, seg=True):
+    """Algorithmic HBM bytes of one step-kernel launch.
+
+    Segmented path (M = N + No <= 64): per env, reads pos of every entity,
+    agent vel, actions, the 16-B counters, the agent contact-candidate masks
+    and the cached obstacle adjacency rows; writes agent pos/vel, the agent
+    node-feature rows (goal/obstacle rows are static within an episode), reward,
+    cost, the new masks, counters, done, edge count and the per-block edge sum.
+    Re-layout at episode end rewrites goal/obstacle pos and static node rows:
+    amortised over the episode length. Generic path (M > 64): no masks, every
+    node-feature row written each step."""
+    E, M = 2 * N + No, N + No
+    if seg:
+        reads = 8 * E + 8 * N + action_bytes * N + 16 + 8 * N + 8 * No
+        writes = 8 * N + 8 * N + 28 * N + 4 * N + 4 * N + 8 * N + 8 * M + 16 + 1 + 4
+        reset = (8 * (E - N) + 28 * (E - N) + 8) / EL
+    else:
+        reads = 8 * E + 8 * N + action_bytes * N + 16
+        writes = 8 * N + 8 * N + 28 * E + 4 * N + 4 * N + 16 + 1 + 4
+        reset = (8 * (E - N) + 8) / EL
+    envs_per_block = 4 * (min(64 // M, 16) if seg else 1)
+    return B * (reads + writes + reset + 4 / envs_per_block)
 
 
-def emit_kernel_bytes(B, N, No, total_edges):
-    """Algorithmic HBM bytes of one gsm_emit_edges_kernel launch."""
-    E = 2 * N + No
-    return B * (8 * E + 4 + 8) + 12 * total_edges
+def emit_kernel_bytes(B, N, No, total_edges, seg=True):
+    """Algorithmic HBM bytes of one edge-emit launch: entity positions (and
+    the adjacency row masks on the segmented path), the env's edge count, the
+    int64 edge_ptr entry and 12 B per edge (src, dst int32 + fp32 distance)."""
+    E, M = 2 * N + No, N + No
+    per_env = 8 * E + 4 + 8 + (8 * M if seg else 0)
+    return B * per_env + 12 * total_edges
+
+
+CONFIGS = {   # BASELINE.json configs runnable as a one-GPU bench line
+    "h": (24, 8192, "BASELINE headline / configs[4] shard"),
+    "c2": (3, 4096, "BASELINE configs[1]"),
+    "c3": (96, 1024, "BASELINE configs[2]"),
+}
 
 
 def cpu_baseline(n_agents, seconds):
@@ -95,12 +120,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=50)
-    ap.add_argument("--n-agents", type=int, default=24)
-    ap.add_argument("--n-envs", type=int, default=8192, help="envs per GPU")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="h",
+                    help="BASELINE config (h = 24 agents x 8192 envs per GPU)")
+    ap.add_argument("--n-agents", type=int, default=None, help="override the config's agents")
+    ap.add_argument("--n-envs", type=int, default=None, help="override the config's envs per GPU")
+    ap.add_argument("--kernel-launches", type=int, default=100,
+                    help="back-to-back launches per kernel for the event-timed roofline")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-timing-events", action="store_true",
-                    help="capture without per-kernel HIP event nodes (roofline then null)")
+    ap.add_argument("--no-kernel-timing", action="store_true", help="skip the roofline timing (null)")
     ap.add_argument("--eager", action="store_true", help="launch steps eagerly instead of HIP graphs")
     args = ap.parse_args()
 
@@ -121,7 +149,9 @@ def main():
     from gsmarl_amd import EnvConfig, GpuBatchEnv
     from gsmarl_amd.distributed import all_reduce_metrics, max_over_ranks, shard_config
 
-    N, B = args.n_agents, args.n_envs
+    N, B, cfg_name = CONFIGS[args.config]
+    N = args.n_agents or N
+    B = args.n_envs or B
     cfg = shard_config(EnvConfig(n_agents=N, n_envs=B, seed=1234), rank, world)
     env = GpuBatchEnv(cfg, dev)
     EL = cfg.episode_length
@@ -133,11 +163,10 @@ def main():
     K, W = args.steps, args.warmup
     chunk = min(K, EL)
     n_chunks, rem = divmod(K, chunk)
-    timing = not args.no_timing_events and not args.eager
     if not args.eager:
         if W > 0:
             env.capture(actions, W, timing=False, slot=2)
-        env.capture(actions, chunk, timing=timing, slot=0)
+        env.capture(actions, chunk, timing=False, slot=0)
         if rem:
             env.capture(actions, rem, timing=False, slot=1)
     # warmup
@@ -178,24 +207,40 @@ def main():
     value = world * B * N * K / elapsed
     ms_per_step = elapsed / K * 1e3
 
+    # Roofline: each kernel's mean launch duration, HIP events (graph event
+    # nodes on the launch stream) around L back-to-back launches of that
+    # kernel alone, after the timed region. Event nodes between kernels would
+    # add their own packet time to every launch.
     roofline = None
-    kern = None
-    if timing:
-        step_ms, emit_ms = env.graph_kernel_ms(0)
-        sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4)
-        eb = emit_kernel_bytes(B, N, cfg.n_obstacles, total_edges)
-        kern = dict(step_kernel_ms=step_ms, emit_kernel_ms=emit_ms,
-                    step_kernel_bytes=sb, emit_kernel_bytes=eb,
-                    step_kernel_gbs=sb / (step_ms * 1e-3) / 1e9,
-                    emit_kernel_gbs=eb / (emit_ms * 1e-3) / 1e9)
+    if not args.no_kernel_timing and not args.eager:
+        L = args.kernel_launches
+        seg = (N + cfg.n_obstacles) <= 64
+        env.capture(actions, L, slot=3, kernels="step", time_ends=True)
+        env.replay(3)
+        torch.cuda.synchronize()
+        step_ms = env.graph_kernel_ms(3)[0]
+        env.capture(None, L, slot=3, kernels="emit", time_ends=True)
+        env.replay(3)
+        torch.cuda.synchronize()
+        emit_ms = env.graph_kernel_ms(3)[1]
+        edges_now = int(env.t["edge_ptr"][B].item())
+        sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4, seg)
+        eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)
+        names = ("gsm_step_seg_kernel", "gsm_emit_seg_kernel") if seg else ("gsm_step_kernel",
+                                                                           "gsm_emit_edges_kernel")
+        kern = {"step": dict(kernel=names[0], ms=step_ms, bytes=sb, gbs=sb / (step_ms * 1e-3) / 1e9),
+                "emit": dict(kernel=names[1], ms=emit_ms, bytes=eb, gbs=eb / (emit_ms * 1e-3) / 1e9)}
         dom = "step" if step_ms >= emit_ms else "emit"
-        ach = kern[f"{dom}_kernel_gbs"]
-        roofline = dict(kernel="gsm_step_kernel" if dom == "step" else "gsm_emit_edges_kernel",
-                        bound="hbm", achieved=round(ach, 1), peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=round(ach / HBM_PEAK_GBS, 4),
-                        algorithmic_bytes_per_launch=int(kern[f"{dom}_kernel_bytes"]),
-                        mean_launch_ms=round(kern[f"{dom}_kernel_ms"], 5),
-                        traffic=pmc_traffic(f"{dom}:N{N}:B{B}"))
+        k = kern[dom]
+        other = kern["emit" if dom == "step" else "step"]
+        roofline = dict(kernel=k["kernel"], bound="hbm", achieved=round(k["gbs"], 1), peak=HBM_PEAK_GBS,
+                        unit="GB/s", frac=round(k["gbs"] / HBM_PEAK_GBS, 4),
+                        traffic=pmc_traffic(f"{dom}:N{N}:B{B}"),
+                        algorithmic_bytes_per_launch=int(k["bytes"]), mean_launch_us=round(k["ms"] * 1e3, 3),
+                        timing=f"HIP events around {L} back-to-back graph launches of the kernel",
+                        other_kernel=dict(kernel=other["kernel"], achieved=round(other["gbs"], 1),
+                                          algorithmic_bytes_per_launch=int(other["bytes"]),
+                                          mean_launch_us=round(other["ms"] * 1e3, 3)))
         log(f"kernels: {json.dumps(kern)}")
 
     cpu = None
@@ -209,7 +254,7 @@ def main():
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: Philox4x32-10 layouts, uniform random discrete actions pre-generated on device",
             "config": {"workload": f"cooperative_navigation {N} agents x {B} envs per GPU "
-                                   f"({N} goals, {cfg.n_obstacles} obstacles; BASELINE headline / configs[4] shard)",
+                                   f"({N} goals, {cfg.n_obstacles} obstacles; {cfg_name})",
                        "n_agents": N, "n_envs_per_gpu": B, "global_envs": world * B,
                        "episode_length": EL, "mean_edges_per_env": round(total_edges / B, 2),
                        "parallelism": f"env-sharded x{world} (no data-path collective)",

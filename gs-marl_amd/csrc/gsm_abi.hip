@@ -26,8 +26,10 @@ struct gsm_handle {
     struct Slot {
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
-        std::vector<hipEvent_t> events;   // 2 per step + 1 when timing
+        std::vector<hipEvent_t> events;   // timing event-record nodes
         int steps = 0;
+        int kern = 0;
+        bool each = false;
     } slots[GSM_GRAPH_SLOTS];
 };
 
@@ -183,6 +185,8 @@ void drop_slot(gsm_handle::Slot &s) {
     s.graph = nullptr;
     s.events.clear();
     s.steps = 0;
+    s.kern = 0;
+    s.each = false;
 }
 
 void drop_graph(gsm_handle *h) {
@@ -279,12 +283,16 @@ int gsm_observe(gsm_handle *h, void *stream) {
 }
 
 int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t stride,
-                      int32_t n_actions, int32_t n_steps, int action_fmt, int with_timing) {
+                      int32_t n_actions, int32_t n_steps, int action_fmt, int flags) {
     if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
     if (!h->bound) return fail(h, GSM_ESTATE, "gsm_bind has not been called");
     if (bad_slot(slot)) return fail(h, GSM_EINVAL, "bad graph slot");
-    if (!actions || n_actions < 1 || n_steps < 1 || stride < 0)
+    int kern = flags & (GSM_GRAPH_STEP | GSM_GRAPH_EMIT);
+    if (!kern) kern = GSM_GRAPH_STEP | GSM_GRAPH_EMIT;
+    const bool each = (flags & GSM_GRAPH_TIME_EACH) != 0, ends = (flags & GSM_GRAPH_TIME_ENDS) != 0;
+    if ((kern & GSM_GRAPH_STEP) && (!actions || n_actions < 1 || stride < 0))
         return fail(h, GSM_EINVAL, "bad capture arguments");
+    if (n_steps < 1) return fail(h, GSM_EINVAL, "n_steps must be >= 1");
     if (action_fmt < GSM_ACT_ONEHOT || action_fmt > GSM_ACT_CONT) return fail(h, GSM_EINVAL, "bad action_fmt");
     gsm_handle::Slot &sl = h->slots[slot];
     drop_slot(sl);
@@ -294,17 +302,19 @@ int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t 
         if (e != hipSuccess) return hip_fail(h, e, "hipStreamCreate");
     }
     // The graph is built node by node (a linear chain) rather than by stream
-    // capture: event-record nodes for per-kernel timing are then explicit
-    // (the capture path of the HIP runtime bundled with PyTorch rejects
+    // capture: event-record nodes for timing are then explicit (the capture
+    // path of the HIP runtime bundled with PyTorch rejects
     // hipEventRecordWithFlags(..., hipEventRecordExternal)).
-    //   [E0] -> step_0 -> [E1] -> emit_0 -> [E2] -> step_1 -> ...
-    if (with_timing) {
-        sl.events.resize(2 * (size_t)n_steps + 1, nullptr);
-        for (auto &ev : sl.events) {
-            e = hipEventCreate(&ev);
-            if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipEventCreate"); }
-        }
+    //   TIME_EACH:  [E0] step_0 [E1] emit_0 [E2] step_1 ...   (events: 2 per step + 1)
+    //   TIME_ENDS:  [E0] step_0 emit_0 step_1 ... [E1]
+    const size_t n_ev = each ? 2 * (size_t)n_steps + 1 : (ends ? 2 : 0);
+    sl.events.resize(n_ev, nullptr);
+    for (auto &ev : sl.events) {
+        e = hipEventCreate(&ev);
+        if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipEventCreate"); }
     }
+    sl.each = each;
+    sl.kern = kern;
     e = hipGraphCreate(&sl.graph, 0);
     if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipGraphCreate"); }
     gsm::DevParams p = h->dp;
@@ -315,11 +325,9 @@ int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t 
     hipGraphNode_t prev = nullptr;
     const char *what = "";
     int at = 0;
-    auto add_event = [&](int k) -> hipError_t {
-        if (!with_timing) return hipSuccess;
+    auto add_event = [&](hipEvent_t ev) -> hipError_t {
         hipGraphNode_t n;
-        const hipError_t r = hipGraphAddEventRecordNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0,
-                                                        sl.events[k]);
+        const hipError_t r = hipGraphAddEventRecordNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0, ev);
         if (r == hipSuccess) prev = n;
         return r;
     };
@@ -338,16 +346,22 @@ int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t 
         return r;
     };
     what = "event node";
-    e = add_event(0);
+    e = n_ev ? add_event(sl.events[0]) : hipSuccess;
     for (int t = 0; t < n_steps && e == hipSuccess; ++t) {
         at = t;
-        p.actions = (const char *)actions + (int64_t)(t % n_actions) * stride;
-        what = "step kernel node";
-        e = add_kernel(gsm::step_kernel_fn(p), gsm::step_kernel_lds(p));
-        if (e == hipSuccess) { what = "event node"; e = add_event(2 * t + 1); }
-        if (e == hipSuccess) { what = "emit kernel node"; e = add_kernel(gsm::emit_kernel_fn(p), gsm::emit_kernel_lds(p)); }
-        if (e == hipSuccess) { what = "event node"; e = add_event(2 * t + 2); }
+        if (kern & GSM_GRAPH_STEP) {
+            p.actions = (const char *)actions + (int64_t)(t % n_actions) * stride;
+            what = "step kernel node";
+            e = add_kernel(gsm::step_kernel_fn(p), gsm::step_kernel_lds(p));
+            if (e == hipSuccess && each) { what = "event node"; e = add_event(sl.events[2 * t + 1]); }
+        }
+        if (e == hipSuccess && (kern & GSM_GRAPH_EMIT)) {
+            what = "emit kernel node";
+            e = add_kernel(gsm::emit_kernel_fn(p), gsm::emit_kernel_lds(p));
+        }
+        if (e == hipSuccess && each) { what = "event node"; e = add_event(sl.events[2 * t + 2]); }
     }
+    if (e == hipSuccess && ends && !each) { what = "event node"; e = add_event(sl.events[1]); }
     if (e != hipSuccess) {
         drop_slot(sl);
         char where[96];
@@ -372,22 +386,36 @@ int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream) {
     return GSM_OK;
 }
 
-int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_ms, float *emit_ms) {
+int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_ms, float *emit_ms, float *total_ms) {
     if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
     if (bad_slot(slot)) return fail(h, GSM_EINVAL, "bad graph slot");
     const gsm_handle::Slot &sl = h->slots[slot];
     if (!sl.exec || sl.events.empty()) return fail(h, GSM_ESTATE, "no timed graph in this slot");
+    float total = 0;
+    hipError_t e = hipEventElapsedTime(&total, sl.events.front(), sl.events.back());
+    if (e != hipSuccess) return hip_fail(h, e, "hipEventElapsedTime");
     double a = 0, b = 0;
-    for (int t = 0; t < sl.steps; ++t) {
-        float x = 0, y = 0;
-        hipError_t e = hipEventElapsedTime(&x, sl.events[2 * t], sl.events[2 * t + 1]);
-        if (e == hipSuccess) e = hipEventElapsedTime(&y, sl.events[2 * t + 1], sl.events[2 * t + 2]);
-        if (e != hipSuccess) return hip_fail(h, e, "hipEventElapsedTime");
-        a += x;
-        b += y;
+    if (sl.each) {
+        for (int t = 0; t < sl.steps; ++t) {
+            float x = 0, y = 0;
+            if (sl.kern & GSM_GRAPH_STEP) e = hipEventElapsedTime(&x, sl.events[2 * t], sl.events[2 * t + 1]);
+            if (e == hipSuccess && (sl.kern & GSM_GRAPH_EMIT))
+                e = hipEventElapsedTime(&y, sl.events[2 * t + ((sl.kern & GSM_GRAPH_STEP) ? 1 : 0)],
+                                        sl.events[2 * t + 2]);
+            if (e != hipSuccess) return hip_fail(h, e, "hipEventElapsedTime");
+            a += x;
+            b += y;
+        }
+        a /= sl.steps;
+        b /= sl.steps;
+    } else {
+        // back-to-back launches of one kind: the mean per launch
+        if (sl.kern == GSM_GRAPH_STEP) a = total / sl.steps;
+        else if (sl.kern == GSM_GRAPH_EMIT) b = total / sl.steps;
     }
-    if (step_ms) *step_ms = (float)(a / sl.steps);
-    if (emit_ms) *emit_ms = (float)(b / sl.steps);
+    if (step_ms) *step_ms = (float)a;
+    if (emit_ms) *emit_ms = (float)b;
+    if (total_ms) *total_ms = total;
     return GSM_OK;
 }
 

@@ -91,8 +91,8 @@ __device__ __forceinline__ int wave_scan(int v) {
         if ((p).stamps && (threadIdx.x & 63) == 0) (p).stamps[(int64_t)(wave_id)*16 + (k)] = t_;  \
     } while (0)
 #else
-#define GSM_STAMP(p, wave_id, k) do { } while (0)
-#define GSM_RSTAMP(p, wave_id, k) do { } while (0)
+#define GSM_STAMP(p, wave_id, k) do { (void)(wave_id); } while (0)
+#define GSM_RSTAMP(p, wave_id, k) do { (void)(wave_id); } while (0)
 #endif
 
 // number of set bits of `mask` below this lane

@@ -15,6 +15,7 @@ ABI_VERSION = 2
 
 GSM_OK, GSM_EINVAL, GSM_EHIP, GSM_ESTATE = 0, -1, -2, -3
 GRAPH_SLOTS = 4
+GRAPH_STEP, GRAPH_EMIT, GRAPH_TIME_EACH, GRAPH_TIME_ENDS = 1, 2, 4, 8
 ACT_ONEHOT, ACT_INDEX, ACT_CONT = 0, 1, 2
 
 
@@ -61,7 +62,8 @@ SIGNATURES = {
     "gsm_observe": (C.c_int, [_P, _P]),
     "gsm_graph_capture": (C.c_int, [_P, C.c_int32, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int, C.c_int]),
     "gsm_graph_launch": (C.c_int, [_P, C.c_int32, _P]),
-    "gsm_graph_kernel_ms": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_float)]),
+    "gsm_graph_kernel_ms": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                      C.POINTER(C.c_float)]),
     "gsm_debug_set_stamps": (C.c_int, [_P, _P]),
     "gsm_destroy": (C.c_int, [_P]),
     "gsm_last_error": (C.c_int, [_P, C.c_char_p, C.c_size_t]),

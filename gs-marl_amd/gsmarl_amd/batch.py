@@ -167,26 +167,39 @@ class GpuBatchEnv:
         return self.observe(sync_edges)
 
     # ------------------------------------------------------------ HIP graph
-    def capture(self, actions_seq: torch.Tensor, n_steps: int, timing: bool = False, slot: int = 0) -> None:
-        """Capture ``n_steps`` steps into HIP graph ``slot``; the j-th captured
-        step uses ``actions_seq[j % len(actions_seq)]`` (a [T, B, N(,k)] device tensor)."""
-        a = actions_seq.contiguous()
-        fmt = self._action_fmt(a[0])
-        stride = a[0].numel() * a.element_size()
+    def capture(self, actions_seq: Optional[torch.Tensor], n_steps: int, timing: bool = False,
+                slot: int = 0, kernels: str = "both", time_ends: bool = False) -> None:
+        """Build HIP graph ``slot`` of ``n_steps`` steps; the j-th step uses
+        ``actions_seq[j % len(actions_seq)]`` (a [T, B, N(,k)] device tensor).
+        kernels: "both", "step" or "emit" (re-emits the current edges).
+        timing: event nodes around every kernel; time_ends: only around the
+        whole graph (per-kernel means over back-to-back launches)."""
+        flags = {"both": 0, "step": _lib.GRAPH_STEP, "emit": _lib.GRAPH_EMIT}[kernels]
+        if timing:
+            flags |= _lib.GRAPH_TIME_EACH
+        if time_ends:
+            flags |= _lib.GRAPH_TIME_ENDS
+        if actions_seq is None:
+            a, fmt, stride, n_act, ptr = None, _lib.ACT_INDEX, 0, 1, None
+        else:
+            a = actions_seq.contiguous()
+            fmt = self._action_fmt(a[0])
+            stride = a[0].numel() * a.element_size()
+            n_act, ptr = a.shape[0], C.c_void_p(a.data_ptr())
         self._graph_actions[slot] = a   # keep alive while the graph exists
-        self._chk(self.lib.gsm_graph_capture(self._h, int(slot), C.c_void_p(a.data_ptr()), stride,
-                                             a.shape[0], int(n_steps), fmt, int(timing)),
-                  "gsm_graph_capture")
+        self._chk(self.lib.gsm_graph_capture(self._h, int(slot), ptr, stride, n_act, int(n_steps), fmt,
+                                             flags), "gsm_graph_capture")
 
     def replay(self, slot: int = 0) -> None:
         self._chk(self.lib.gsm_graph_launch(self._h, int(slot), self._stream()), "gsm_graph_launch")
 
     def graph_kernel_ms(self, slot: int = 0):
-        """(mean step-kernel ms, mean edge-emit-kernel ms) of the last timed replay."""
-        a, b = C.c_float(), C.c_float()
-        self._chk(self.lib.gsm_graph_kernel_ms(self._h, int(slot), C.byref(a), C.byref(b)),
+        """(mean step-kernel ms, mean emit-kernel ms, whole-graph ms) of the
+        last replay of a timed graph."""
+        a, b, c = C.c_float(), C.c_float(), C.c_float()
+        self._chk(self.lib.gsm_graph_kernel_ms(self._h, int(slot), C.byref(a), C.byref(b), C.byref(c)),
                   "gsm_graph_kernel_ms")
-        return a.value, b.value
+        return a.value, b.value, c.value
 
     # ---------------------------------------------------------------- metrics
     def episode_metrics(self) -> torch.Tensor:

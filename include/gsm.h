@@ -145,18 +145,26 @@ int gsm_step(gsm_handle *h, const void *actions, int action_fmt, void *stream);
  * state buffers, e.g. set_state). */
 int gsm_observe(gsm_handle *h, void *stream);
 
-/* Capture n_steps gsm_step launches into HIP graph `slot` (0..GSM_GRAPH_SLOTS-1;
- * actions for the j-th captured step at actions + (j % n_actions) *
- * action_stride_bytes). with_timing != 0 brackets each step kernel and each
- * edge-emit kernel with HIP event records (read by gsm_graph_kernel_ms).
+/* Build HIP graph `slot` (0..GSM_GRAPH_SLOTS-1) of n_steps steps; the j-th
+ * step reads its actions at actions + (j % n_actions) * action_stride_bytes.
+ * flags: which kernels each step runs (GSM_GRAPH_STEP | GSM_GRAPH_EMIT; 0 =
+ * both) and optional HIP event-record nodes: GSM_GRAPH_TIME_EACH brackets
+ * every kernel, GSM_GRAPH_TIME_ENDS brackets the whole graph (per-kernel
+ * means over back-to-back launches, no event nodes between kernels).
+ * A graph running only GSM_GRAPH_EMIT re-emits the current step's edges.
  * Graphs are dropped by gsm_bind and by a reseed to a different seed. */
 #define GSM_GRAPH_SLOTS 4
+#define GSM_GRAPH_STEP 1
+#define GSM_GRAPH_EMIT 2
+#define GSM_GRAPH_TIME_EACH 4
+#define GSM_GRAPH_TIME_ENDS 8
 int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t action_stride_bytes,
-                      int32_t n_actions, int32_t n_steps, int action_fmt, int with_timing);
+                      int32_t n_actions, int32_t n_steps, int action_fmt, int flags);
 int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream);
 /* After a timed launch of `slot` has completed: mean duration (ms) of the
- * step kernel and of the edge-emit kernel over the captured steps. */
-int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_mean_ms, float *emit_mean_ms);
+ * step and emit kernels (TIME_EACH), and the whole graph (both flags). */
+int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_mean_ms, float *emit_mean_ms,
+                        float *total_ms);
 
 /* Diagnostics: device buffer (uint64 [2 * n_blocks * 4][16]) that libraries
  * built with -DGSM_STAMPS fill with per-wave phase timestamps; ignored by the

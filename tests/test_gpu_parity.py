@@ -249,13 +249,41 @@ def test_graph_replay_equals_eager_and_deterministic():
     for k in ("pos", "vel", "step_count", "episode", "node_feat", "reward", "cost", "edge_ptr",
               "edge_index", "edge_attr", "ep_acc", "ep_last"):
         assert torch.equal(eager[k], env.t[k]), k
-    a, b = env.graph_kernel_ms()
-    assert a > 0 and b > 0
+    a, b, tot = env.graph_kernel_ms()
+    assert a > 0 and b > 0 and tot >= T * (a + b) * 0.99
     env.reset(seed=5)
     env.replay()
     torch.cuda.synchronize()
     assert torch.equal(eager["edge_index"], env.t["edge_index"])
     assert torch.equal(eager["pos"], env.t["pos"])
+
+
+def test_kernel_only_graphs():
+    """Roofline timing graphs: a step-only graph advances the physics exactly
+    like eager steps; an emit-only graph re-emits the same edges (idempotent)."""
+    env, ocfg = _env(n_agents=24, n_envs=512, episode_length=1000)
+    T = 12
+    acts = torch.randint(0, 5, (T, 512, 24), dtype=torch.int32, device=DEV)
+    env.reset(seed=8)
+    for t in range(T):
+        env.step(acts[t], sync_edges=False)
+    eager = {k: v.clone() for k, v in env.t.items()}
+    env.reset(seed=8)
+    env.capture(acts, T, slot=3, kernels="step", time_ends=True)
+    env.replay(3)
+    torch.cuda.synchronize()
+    for k in ("pos", "vel", "step_count", "reward", "cost", "node_feat", "edge_count"):
+        assert torch.equal(eager[k], env.t[k]), k
+    s_ms, e_ms, tot = env.graph_kernel_ms(3)
+    assert s_ms > 0 and e_ms == 0 and abs(s_ms * T - tot) < 1e-6 * T + 1e-3
+    env.capture(None, 5, slot=3, kernels="emit", time_ends=True)
+    env.replay(3)
+    torch.cuda.synchronize()
+    n = int(eager["edge_ptr"][-1])   # beyond it: stale entries of earlier steps
+    assert torch.equal(eager["edge_ptr"], env.t["edge_ptr"])
+    assert torch.equal(eager["edge_index"][:, :n], env.t["edge_index"][:, :n])
+    assert torch.equal(eager["edge_attr"][:n], env.t["edge_attr"][:n])
+    assert env.graph_kernel_ms(3)[1] > 0
 
 
 def test_headline_size_properties():
