@@ -71,11 +71,61 @@ def emit_kernel_bytes(B, N, No, total_edges, seg=True):
     return B * per_env + 12 * total_edges
 
 
+def ragged_kernel_bytes(env, EL, action_bytes, total_edges):
+    """Algorithmic HBM bytes of one ragged step / emit launch, summed over the
+    batch's actual env shapes (N_env agents, T targets, M colliders).
+
+    step: reads collider + target positions, agent vel, actions, counters and
+    the shape word; writes agent pos/vel, 6 node-feature floats per agent,
+    reward/cost/assign (N_max each), the M row masks, counters, done, edge
+    count; re-layout (all E_max rows of pos and node features, N_max vel)
+    amortised over the episode. emit: reads all E_max positions, the M row
+    masks, edge count and shape; writes edge_ptr and 12 B per edge."""
+    import numpy as np
+    sh = env.t["env_shape"].cpu().numpy()
+    n, scn = (sh & 0xFF).astype(np.int64), sh >> 8
+    T = np.where(scn == 0, n, np.where(scn == 1, 1, 2))
+    M = n + np.where(scn == 0, n, 0)
+    Nmax, Emax = env.N, env.E
+    reads = 8 * (M + T) + 8 * n + action_bytes * n + 16 + 4
+    writes = 8 * n + 8 * n + 24 * n + 12 * Nmax + 8 * M + 16 + 1 + 4
+    reset = (8 * Emax + 28 * Emax + 8 * Nmax + 4) / EL
+    step = float((reads + writes + reset).sum()) + 4 * len(n) / 4
+    emit = float((8 * Emax + 8 * M + 4 + 4 + 8).sum()) + 12 * total_edges
+    return step, emit
+
+
 CONFIGS = {   # BASELINE.json configs runnable as a one-GPU bench line
-    "h": (24, 8192, "BASELINE headline / configs[4] shard"),
-    "c2": (3, 4096, "BASELINE configs[1]"),
-    "c3": (96, 1024, "BASELINE configs[2]"),
+    "h": dict(scenario="navigation", n_agents=24, n_envs=8192, desc="BASELINE headline / configs[4] shard"),
+    "c2": dict(scenario="navigation", n_agents=3, n_envs=4096, desc="BASELINE configs[1]"),
+    "c3": dict(scenario="navigation", n_agents=96, n_envs=1024, desc="BASELINE configs[2]"),
+    "c4": dict(scenario="mixed", n_agents=24, n_envs=8192, n_agents_min=3,
+               desc="BASELINE configs[3]: mixed navigation/polygon/line, N_env in {3..24}"),
 }
+
+
+def cpu_baseline_ragged(cfg, seconds):
+    """Ragged restatement (oracle/ragged_ref.py, per-env NumPy + the scipy-
+    equivalent LSA restatement) on one host core, over a 30-env sample."""
+    import numpy as np
+    from oracle import ragged_ref as rr
+    keys = set(rr.br.DEFAULTS) | set(rr.RAGGED_DEFAULTS)
+    rcfg = rr.make_cfg(**{k: v for k, v in cfg.to_dict().items() if k in keys})
+    rcfg.n_envs = 30
+    st = rr.new_state(rcfg)
+    rng = np.random.default_rng(0)
+    agents = int(st["n"].sum())
+    steps = 0
+    t0 = time.perf_counter()
+    while True:
+        st, _ = rr.step(rcfg, st, rng.integers(0, 5, (30, cfg.n_agents)), 1, np.float64)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            break
+    return dict(value=steps * agents / el, unit="agent-steps/s", cores=1, kind="port",
+                sample=f"30 envs ({agents} agents) x {steps} steps ({el:.1f} s) of oracle/ragged_ref.py step "
+                       f"(per-env NumPy, fp64, per-step assignment via oracle/lsa_ref.py), 1 host core")
 
 
 def cpu_baseline(n_agents, seconds):
@@ -149,10 +199,14 @@ def main():
     from gsmarl_amd import EnvConfig, GpuBatchEnv
     from gsmarl_amd.distributed import all_reduce_metrics, max_over_ranks, shard_config
 
-    N, B, cfg_name = CONFIGS[args.config]
-    N = args.n_agents or N
-    B = args.n_envs or B
-    cfg = shard_config(EnvConfig(n_agents=N, n_envs=B, seed=1234), rank, world)
+    spec = dict(CONFIGS[args.config])
+    cfg_name = spec.pop("desc")
+    if args.n_agents:
+        spec["n_agents"] = args.n_agents
+    if args.n_envs:
+        spec["n_envs"] = args.n_envs
+    N, B = spec["n_agents"], spec["n_envs"]
+    cfg = shard_config(EnvConfig(seed=1234, **spec), rank, world)
     env = GpuBatchEnv(cfg, dev)
     EL = cfg.episode_length
     gen = torch.Generator(device=dev)
@@ -204,7 +258,12 @@ def main():
     elapsed = max_over_ranks(elapsed, device=dev) if world > 1 else elapsed
 
     total_edges = int(env.t["edge_ptr"][B].item())
-    value = world * B * N * K / elapsed
+    # agents per step on this rank (ragged: sum of N_env), summed over ranks
+    agents = int((env.t["env_shape"] & 0xFF).sum().item()) if cfg.ragged else B * N
+    if world > 1:
+        agents = int(all_reduce_metrics(torch.tensor([float(agents), 0.0, 0.0], dtype=torch.float64,
+                                                     device=dev))[0].item())
+    value = agents * K / elapsed
     ms_per_step = elapsed / K * 1e3
 
     # Roofline: each kernel's mean launch duration, HIP events (graph event
@@ -214,7 +273,7 @@ def main():
     roofline = None
     if not args.no_kernel_timing and not args.eager:
         L = args.kernel_launches
-        seg = (N + cfg.n_obstacles) <= 64
+        seg = (N + cfg.n_obstacles) <= 64 and not cfg.ragged
         env.capture(actions, L, slot=3, kernels="step", time_ends=True)
         env.replay(3)
         torch.cuda.synchronize()
@@ -224,10 +283,14 @@ def main():
         torch.cuda.synchronize()
         emit_ms = env.graph_kernel_ms(3)[1]
         edges_now = int(env.t["edge_ptr"][B].item())
-        sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4, seg)
-        eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)
-        names = ("gsm_step_seg_kernel", "gsm_emit_seg_kernel") if seg else ("gsm_step_kernel",
-                                                                           "gsm_emit_edges_kernel")
+        if cfg.ragged:
+            sb, eb = ragged_kernel_bytes(env, EL, 4, edges_now)
+            names = ("gsm_step_ragged_kernel", "gsm_emit_ragged_kernel")
+        else:
+            sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4, seg)
+            eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)
+            names = ("gsm_step_seg_kernel", "gsm_emit_seg_kernel") if seg else ("gsm_step_kernel",
+                                                                               "gsm_emit_edges_kernel")
         kern = {"step": dict(kernel=names[0], ms=step_ms, bytes=sb, gbs=sb / (step_ms * 1e-3) / 1e9),
                 "emit": dict(kernel=names[1], ms=emit_ms, bytes=eb, gbs=eb / (emit_ms * 1e-3) / 1e9)}
         dom = "step" if step_ms >= emit_ms else "emit"
@@ -245,7 +308,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(N, args.cpu_seconds)
+        cpu = cpu_baseline_ragged(cfg, args.cpu_seconds) if cfg.ragged else cpu_baseline(N, args.cpu_seconds)
 
     if rank == 0:
         line = {
@@ -253,9 +316,11 @@ def main():
             "steps": K, "warmup": W, "ms_per_step": round(ms_per_step, 5), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
             "data": "synthetic: Philox4x32-10 layouts, uniform random discrete actions pre-generated on device",
-            "config": {"workload": f"cooperative_navigation {N} agents x {B} envs per GPU "
-                                   f"({N} goals, {cfg.n_obstacles} obstacles; {cfg_name})",
-                       "n_agents": N, "n_envs_per_gpu": B, "global_envs": world * B,
+            "config": {"workload": (f"cooperative_navigation {N} agents x {B} envs per GPU "
+                                    f"({N} goals, {cfg.n_obstacles} obstacles; {cfg_name})") if not cfg.ragged
+                       else f"{cfg.scenario} up to {N} agents x {B} envs per GPU ({cfg_name})",
+                       "scenario": cfg.scenario, "n_agents": N, "n_envs_per_gpu": B, "global_envs": world * B,
+                       "agents_per_step": agents,
                        "episode_length": EL, "mean_edges_per_env": round(total_edges / B, 2),
                        "parallelism": f"env-sharded x{world} (no data-path collective)",
                        "launch": "eager" if args.eager else "hip-graph per 100-step episode"},

@@ -58,14 +58,40 @@ int check_config(const gsm_config *c, std::string *why) {
                std::to_string(c->abi_version) + ")";
         return GSM_EINVAL;
     }
-    if (c->scenario != GSM_SCEN_NAVIGATION) { *why = "unsupported scenario"; return GSM_EINVAL; }
+    if (c->scenario < GSM_SCEN_NAVIGATION || c->scenario > GSM_SCEN_MIXED) {
+        *why = "unsupported scenario";
+        return GSM_EINVAL;
+    }
     if (c->n_envs < 1) { *why = "n_envs must be >= 1"; return GSM_EINVAL; }
     if (c->n_agents < 1 || c->n_agents > 1024) { *why = "n_agents must be in [1, 1024]"; return GSM_EINVAL; }
     if (c->n_obstacles < 0 || c->n_obstacles > 1024) { *why = "n_obstacles must be in [0, 1024]"; return GSM_EINVAL; }
     if (c->episode_length < 1) { *why = "episode_length must be >= 1"; return GSM_EINVAL; }
-    if (!(c->dt > 0) || !(c->mass > 0) || !(c->contact_margin > 0) || !(c->world_half > 0)) {
-        *why = "dt, mass, contact_margin and world_half must be > 0";
+    const bool ragged = c->scenario != GSM_SCEN_NAVIGATION;
+    if (!(c->dt > 0) || !(c->mass > 0) || !(c->contact_margin > 0)) {
+        *why = "dt, mass and contact_margin must be > 0";
         return GSM_EINVAL;
+    }
+    if (ragged ? !(c->world_half >= 0) : !(c->world_half > 0)) {
+        *why = "world_half must be > 0 (ragged scenarios: >= 0, 0 = sqrt(N_env/3) per env)";
+        return GSM_EINVAL;
+    }
+    if (ragged) {
+        if (c->n_agents > GSM_RAGGED_MAX_AGENTS) {
+            *why = "polygon/line/mixed: n_agents must be <= GSM_RAGGED_MAX_AGENTS (32)";
+            return GSM_EINVAL;
+        }
+        if (c->scenario == GSM_SCEN_MIXED ? c->n_obstacles != c->n_agents : c->n_obstacles != 0) {
+            *why = "mixed needs n_obstacles == n_agents (navigation envs); polygon/line need n_obstacles == 0";
+            return GSM_EINVAL;
+        }
+        if (c->scenario == GSM_SCEN_MIXED && (c->n_agents_min < 1 || c->n_agents_min > c->n_agents)) {
+            *why = "mixed needs 1 <= n_agents_min <= n_agents";
+            return GSM_EINVAL;
+        }
+        if (!(c->formation_radius >= 0) || !isfinite(c->formation_radius)) {
+            *why = "formation_radius must be a finite value >= 0";
+            return GSM_EINVAL;
+        }
     }
     if (!(c->damping >= 0 && c->damping <= 1)) { *why = "damping must be in [0, 1]"; return GSM_EINVAL; }
     if (!(c->sense_radius >= 0) || !(c->contact_cutoff > 0)) {
@@ -76,8 +102,12 @@ int check_config(const gsm_config *c, std::string *why) {
 }
 
 // kernel family and envs per wave for a config
-void choose_path(int M, int *path, int *G) {
-    if (M <= gsm::kWave) {
+void choose_path(const gsm_config *c, int *path, int *G) {
+    const int M = c->n_agents + c->n_obstacles;
+    if (c->scenario != GSM_SCEN_NAVIGATION) {
+        *path = gsm::kPathRagged;
+        *G = 1;
+    } else if (M <= gsm::kWave) {
         *path = gsm::kPathSeg;
         int g = gsm::kWave / M;
         *G = g > gsm::kMaxSegEnvsPerWave ? gsm::kMaxSegEnvsPerWave : g;
@@ -87,16 +117,33 @@ void choose_path(int M, int *path, int *G) {
     }
 }
 
+// target rows per env: navigation goals = N, polygon centre 1, line ends 2,
+// mixed = N (its navigation envs)
+int targets_of(const gsm_config *c) {
+    switch (c->scenario) {
+        case GSM_SCEN_POLYGON: return 1;
+        case GSM_SCEN_LINE: return 2;
+        default: return c->n_agents;
+    }
+}
+
 void fill_sizes(const gsm_config *c, gsm_sizes *s) {
-    const int N = c->n_agents, No = c->n_obstacles, M = N + No;
+    const int N = c->n_agents, No = c->n_obstacles, M = N + No, T = targets_of(c);
     int path, G;
-    choose_path(M, &path, &G);
-    s->n_entities = 2 * N + No;
+    choose_path(c, &path, &G);
+    s->n_entities = N + T + No;
     s->node_feat_dim = 7;
     s->obs_dim = 6;
     s->envs_per_block = gsm::kWavesPerBlock * G;
     s->n_blocks = (c->n_envs + s->envs_per_block - 1) / s->envs_per_block;
-    s->max_edges_per_env = M * (M - 1) + 2 * N;
+    // radius edges among colliders + the agent <-> target edges (2 per agent
+    // per target it is tied to: own goal / centre: 1, line ends: 2)
+    int max_edges = M * (M - 1) + 2 * N;
+    if (c->scenario == GSM_SCEN_LINE) max_edges = N * (N - 1) + 4 * N;
+    if (c->scenario == GSM_SCEN_MIXED && N * (N - 1) + 4 * N > max_edges) max_edges = N * (N - 1) + 4 * N;
+    s->max_edges_per_env = max_edges;
+    s->n_colliders = M;
+    s->n_targets = T;
     s->edge_capacity = (int64_t)c->n_envs * s->max_edges_per_env;
 }
 
@@ -107,9 +154,12 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
     p->B = c->n_envs;
     p->N = N;
     p->No = No;
-    p->E = 2 * N + No;
+    p->T = targets_of(c);
+    p->E = N + p->T + No;
     p->M = N + No;
-    choose_path(p->M, &p->path, &p->G);
+    p->scenario = c->scenario;
+    p->n_min = c->scenario == GSM_SCEN_MIXED ? c->n_agents_min : N;
+    choose_path(c, &p->path, &p->G);
     // generic path: N*S lanes of the wave share the contact loop
     int S = N <= gsm::kWave ? gsm::kWave / N : 1;
     if (S > p->M) S = p->M;
@@ -121,7 +171,11 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
     p->seed_lo = (uint32_t)(c->seed & 0xFFFFFFFFull);
     p->seed_hi = (uint32_t)(c->seed >> 32);
     p->env_base = c->env_base;
-    if (p->path == gsm::kPathSeg) {
+    if (p->path == gsm::kPathRagged) {
+        // assignment cost matrix [N][N] fp32 + staged entity positions [E]
+        p->wave_lds_step = align16(4 * N * N + 8 * p->E);
+        p->wave_lds_emit = align16(8 * p->E);
+    } else if (p->path == gsm::kPathSeg) {
         // positions + staged node-feature rows of the wave's G envs
         p->wave_lds_step = align16(8 * p->G * p->E + 28 * p->G * p->E);
         p->wave_lds_emit = align16(8 * p->G * p->E);
@@ -132,6 +186,8 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
     const float L = c->world_half;
     p->L = L;
     p->twoL = L * 2.0f;
+    p->fixed_L = p->path == gsm::kPathRagged ? (L > 0.0f ? L : 0.0f) : L;
+    p->form_r = c->formation_radius;
     p->dt = c->dt;
     p->omd = 1.0f - c->damping;
     p->mass = c->mass;
@@ -238,6 +294,13 @@ int gsm_bind(gsm_handle *h, const gsm_buffers *b) {
                          b->row_mask, b->contact_mask};
     for (const void *q : req)
         if (!q) return fail(h, GSM_EINVAL, "a required buffer pointer is NULL");
+    const bool ragged = h->dp.path == gsm::kPathRagged;
+    if (ragged && (!b->env_shape || !b->assign))
+        return fail(h, GSM_EINVAL, "polygon/line/mixed need the env_shape and assign buffers");
+    if (ragged) {
+        const hipError_t e = gsm::upload_ragged_tables();
+        if (e != hipSuccess) return hip_fail(h, e, "ragged constant tables");
+    }
     if (((uintptr_t)b->pos | (uintptr_t)b->vel | (uintptr_t)b->ep_acc | (uintptr_t)b->ep_last) & 7)
         return fail(h, GSM_EINVAL, "pos/vel/ep_acc/ep_last must be 8-byte aligned");
     gsm::DevParams &p = h->dp;
@@ -258,6 +321,8 @@ int gsm_bind(gsm_handle *h, const gsm_buffers *b) {
     p.edge_attr = b->edge_attr;
     p.row_mask = b->row_mask;
     p.contact_mask = b->contact_mask;
+    p.env_shape = b->env_shape;
+    p.assign = b->assign;
     h->bound = true;
     drop_graph(h);   // a captured graph holds the old pointers
     return GSM_OK;

@@ -8,7 +8,10 @@ namespace gsm {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;              // one env per wave
 constexpr int kBlock = kWave * kWavesPerBlock;
-enum : int32_t { kPathGeneric = 0, kPathSeg = 1 };
+enum : int32_t { kPathGeneric = 0, kPathSeg = 1, kPathRagged = 2 };
+enum : int32_t { kScnNav = 0, kScnPolygon = 1, kScnLine = 2, kScnMixed = 3 };
+constexpr int kRaggedMaxAgents = 32;                                  // = GSM_RAGGED_MAX_AGENTS
+constexpr int kRaggedTable = kRaggedMaxAgents * (kRaggedMaxAgents + 1) / 2;   // rows n = 1..32
 constexpr int kMaxSegEnvsPerWave = 16;   // keeps a block's envs (4G) within one wave's lanes
 
 // Everything a launch needs, passed by value (kernarg segment, < 4 KB).
@@ -17,13 +20,18 @@ constexpr int kMaxSegEnvsPerWave = 16;   // keeps a block's envs (4G) within one
 struct DevParams {
     int32_t B, N, No, E, M, S, EL, auto_reset, shared_reward;
     int32_t mode, action_fmt, reseed;
-    int32_t path;          // kPathSeg (M <= 64) or kPathGeneric
+    int32_t path;          // kPathSeg (M <= 64), kPathGeneric or kPathRagged
+    int32_t scenario;      // ragged: kScnPolygon / kScnLine / kScnMixed
+    int32_t T;             // ragged: target rows per env (T_max); N, No, E, M are the padded maxima
+    int32_t n_min;         // ragged mixed: smallest N_env
     int32_t G;             // envs per wave (segmented path), 1 otherwise
     uint32_t seed_lo, seed_hi;
     int64_t env_base;
     int32_t wave_lds_step, wave_lds_emit;      // bytes of LDS per wave
     float dt, omd, mass, inv_mass, cf, k, inv_k, sens, max_speed, L, twoL, R2;
     float dmin_aa, dmin_ao, dmin2_aa, dmin2_ao, cut2_aa, cut2_ao;
+    float form_r;          // polygon radius
+    float fixed_L;         // ragged: world_half > 0 -> every env's half-width, else 0 (per-N table)
     // caller-owned device buffers (see gsm.h gsm_buffers)
     float2 *pos, *vel;
     int32_t *step_count, *episode;
@@ -36,6 +44,8 @@ struct DevParams {
     float *edge_attr;
     uint64_t *row_mask;       // [B][M] radius row masks (segmented path)
     uint64_t *contact_mask;   // [B][N] contact candidates (segmented path)
+    int32_t *env_shape;       // [B] ragged: N_env | scenario << 8
+    int32_t *assign;          // [B][N] ragged: LSA slot per agent
     int64_t edge_capacity;
     const void *actions;
     const uint8_t *env_mask;
@@ -51,6 +61,11 @@ const void *step_kernel_fn(const DevParams &p);
 const void *emit_kernel_fn(const DevParams &p);
 const void *step_seg_kernel_fn(const DevParams &p);
 const void *emit_seg_kernel_fn(const DevParams &p);
+const void *step_ragged_kernel_fn();
+const void *emit_ragged_kernel_fn();
+// ragged path: per-device constant tables (unit circle, line fractions,
+// half-widths) computed on the host with libm; uploaded once per device.
+hipError_t upload_ragged_tables();
 size_t step_kernel_lds(const DevParams &p);
 size_t emit_kernel_lds(const DevParams &p);
 hipError_t launch_step_kernel(const DevParams &p, hipStream_t s);

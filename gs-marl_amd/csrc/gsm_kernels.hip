@@ -337,9 +337,11 @@ int grid_blocks(const DevParams &p) {
     return (p.B + per_block - 1) / per_block;
 }
 const void *step_kernel_fn(const DevParams &p) {
+    if (p.path == kPathRagged) return step_ragged_kernel_fn();
     return p.path == kPathSeg ? step_seg_kernel_fn(p) : reinterpret_cast<const void *>(&gsm_step_kernel);
 }
 const void *emit_kernel_fn(const DevParams &p) {
+    if (p.path == kPathRagged) return emit_ragged_kernel_fn();
     return p.path == kPathSeg ? emit_seg_kernel_fn(p) : reinterpret_cast<const void *>(&gsm_emit_edges_kernel);
 }
 size_t step_kernel_lds(const DevParams &p) { return (size_t)kWavesPerBlock * p.wave_lds_step + 16; }

@@ -14,7 +14,7 @@
 
 namespace gsm {
 
-enum : uint32_t { kTagLayout = 0u, kTagActions = 1u };
+enum : uint32_t { kTagLayout = 0u, kTagActions = 1u, kTagShape = 2u };
 
 struct Philox4 { uint32_t x0, x1, x2, x3; };
 

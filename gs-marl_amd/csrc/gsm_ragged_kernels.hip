@@ -1,0 +1,557 @@
+// gsm_ragged_kernels.hip — ragged batches: navigation, polygon and line envs
+// with per-env agent counts in one padded batch (SURVEY.md §8 row a12,
+// config C4; semantics in oracle/ragged_ref.py and DESIGN.md §3).
+//
+//  gsm_step_ragged_kernel  one wave64 per env (N_env <= 32, colliders <= 64).
+//                          Lane l holds collider l (agents, then navigation
+//                          obstacles) and target l (goal / centre / line end).
+//                          World.step physics as the other paths; then, for
+//                          polygon/line, the per-step linear sum assignment
+//                          of agents to formation slots (scipy's
+//                          shortest-augmenting-path solver, restated in
+//                          oracle/lsa_ref.py) run one column per lane in
+//                          float64 so the assignment equals scipy's, ties
+//                          included; reward, collision cost, auto-reset,
+//                          node features, radius row masks, edge count.
+//  gsm_emit_ragged_kernel  same env->wave mapping: per-lane row emission from
+//                          the row masks, the agent<->target edges inserted
+//                          in entity order.
+//
+// Storage per env (E = N_max + T_max + O_max rows): agents [0, N_max),
+// targets [N_max, N_max + T_max), obstacles [N_max + T_max, E); rows past the
+// env's own counts are padding (node type -1, position 0).
+#include <math.h>
+
+#include <mutex>
+#include <vector>
+
+#include "gsm_device.h"
+
+namespace gsm {
+
+__constant__ float2 c_unit[kRaggedTable];           // (cos, sin)(2*pi*j/n) at tri(n) + j
+__constant__ float c_linet[kRaggedTable];           // j/(n-1) (n == 1: 0.5) at tri(n) + j
+__constant__ float c_halfw[kRaggedMaxAgents + 1];   // sqrt(n/3)
+
+__host__ __device__ __forceinline__ int tri(int n) { return n * (n - 1) / 2; }
+
+__device__ __forceinline__ float rl_f(float v, int l) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ float2 rl_f2(float2 v, int l) { return make_float2(rl_f(v.x, l), rl_f(v.y, l)); }
+__device__ __forceinline__ double rl_d(double v, int l) {
+    const long long bits = __double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)bits, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(bits >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// reductions over lanes [0, 32) (the assignment never uses more), uniform result
+__device__ __forceinline__ double min32(double v) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) {
+        const double w = __shfl_xor(v, o);
+        v = w < v ? w : v;
+    }
+    return rl_d(v, 0);
+}
+__device__ __forceinline__ int max32(int v) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v = max(v, __shfl_xor(v, o));
+    return __builtin_amdgcn_readlane(v, 0);
+}
+__device__ __forceinline__ int min32(int v) {
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v = min(v, __shfl_xor(v, o));
+    return __builtin_amdgcn_readlane(v, 0);
+}
+__device__ __forceinline__ int first_lane(uint64_t m) { return __builtin_ctzll(m); }
+
+struct RShape {
+    int N, scn, T, O, M, Tper;   // agents, scenario, targets, obstacles, colliders, targets per agent
+    float L, twoL;               // layout half-width
+};
+
+__device__ __forceinline__ RShape make_shape(const DevParams &p, int N, int scn) {
+    RShape s;
+    s.N = N;
+    s.scn = scn;
+    s.T = scn == kScnNav ? N : (scn == kScnPolygon ? 1 : 2);
+    s.O = scn == kScnNav ? N : 0;
+    s.M = N + s.O;
+    s.Tper = scn == kScnLine ? 2 : 1;
+    s.L = p.fixed_L > 0.0f ? p.fixed_L : c_halfw[N];
+    s.twoL = s.L * 2.0f;
+    return s;
+}
+
+// N_env and scenario of global env id gid (oracle/ragged_ref.py: env_shapes)
+__device__ __forceinline__ RShape draw_shape(const DevParams &p, int b) {
+    const int64_t gid = p.env_base + b;
+    int N = p.N, scn = p.scenario;
+    if (p.scenario == kScnMixed) {
+        const Philox4 x = philox4x32_10(0u, 0u, (uint32_t)gid, kTagShape, p.seed_lo, p.seed_hi);
+        N = p.n_min + (int)(((uint64_t)x.x0 * (uint64_t)(p.N - p.n_min + 1)) >> 32);
+        scn = (int)((uint64_t)gid % 3u);
+    }
+    return make_shape(p, N, scn);
+}
+
+__device__ __forceinline__ float2 layout_at(const DevParams &p, const RShape &s, uint32_t gid, uint32_t ep,
+                                            uint32_t e) {
+    const Philox4 x = philox4x32_10(e, ep, gid, kTagLayout, p.seed_lo, p.seed_hi);
+    return make_float2(u01(x.x0) * s.twoL - s.L, u01(x.x1) * s.twoL - s.L);
+}
+
+// storage row of collider l (agents, then obstacles)
+__device__ __forceinline__ int collider_row(const DevParams &p, const RShape &s, int l) {
+    return l < s.N ? l : p.N + p.T + (l - s.N);
+}
+
+// slot j (< N) of a polygon/line env from its target positions (lanes 0/1)
+__device__ __forceinline__ float2 slot_of(const DevParams &p, const RShape &s, int lane, float2 tp) {
+    const int j = lane < s.N ? lane : 0;
+    if (s.scn == kScnPolygon) {
+        const float2 c = rl_f2(tp, 0);
+        const float2 u = c_unit[tri(s.N) + j];
+        const float ox = p.form_r * u.x, oy = p.form_r * u.y;
+        return make_float2(c.x + ox, c.y + oy);
+    }
+    const float2 l0 = rl_f2(tp, 0), l1 = rl_f2(tp, 1);
+    const float tj = c_linet[tri(s.N) + j];
+    const float ex = l1.x - l0.x, ey = l1.y - l0.y;
+    return make_float2(l0.x + ex * tj, l0.y + ey * tj);
+}
+
+// Square linear sum assignment of N <= 32 agents (rows) to N slots (columns),
+// scipy's rectangular_lsap recurrence (oracle/lsa_ref.py) with lane k holding
+// row k and column k. C[i][j] = |p_i - slot_j| in fp32 (staged in LDS),
+// all dual arithmetic in float64 in scipy's operation order. Returns the
+// lane's column (row `lane`), and its cost in *own.
+__device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, float *own) {
+    const bool col = lane < N;
+    for (int i = 0; i < N; ++i) {
+        const float2 pi = rl_f2(pa, i);
+        if (col) {
+            const float dx = pi.x - slot.x, dy = pi.y - slot.y;
+            s_cost[i * N + lane] = sqrtf(dx * dx + dy * dy);
+        }
+    }
+    wave_sync();
+    const double kInf = __builtin_inf();
+    double u = 0.0, v = 0.0;
+    int col4row = -1, row4col = -1;
+    for (int cur = 0; cur < N; ++cur) {
+        double spc = kInf;
+        int path = -1;
+        bool SR = false, SC = false;
+        int rpos = N - 1 - lane;     // position in scipy's `remaining` list (filled in reverse)
+        int nrem = N;
+        double minVal = 0.0;
+        int i = cur, sink = -1;
+        // a square problem reaches a free column within N scans; the bound
+        // only guarantees termination should the invariants ever break
+        for (int guard = 0; sink < 0 && guard < N; ++guard) {
+            if (lane == i) SR = true;
+            const double ui = rl_d(u, i);
+            const bool rem = col && !SC;
+            if (rem) {
+                const double r = minVal + (double)s_cost[i * N + lane] - ui - v;
+                if (r < spc) {
+                    path = i;
+                    spc = r;
+                }
+            }
+            const double m = min32(rem ? spc : kInf);
+            const bool cand = rem && spc == m;
+            const bool fre = cand && row4col == -1;
+            if (!__ballot(cand)) break;
+            // scipy scans `remaining` in order and keeps the first minimum
+            // unless a later equal one is unassigned: the last unassigned
+            // minimum in scan order if any, else the first minimum.
+            int jsel;
+            if (__ballot(fre)) {
+                const int k = max32(fre ? rpos : -1);
+                jsel = first_lane(__ballot(fre && rpos == k));
+            } else {
+                const int k = min32(cand ? rpos : 1 << 30);
+                jsel = first_lane(__ballot(cand && rpos == k));
+            }
+            minVal = m;
+            const int r4c = __builtin_amdgcn_readlane(row4col, jsel);
+            const int at = __builtin_amdgcn_readlane(rpos, jsel);
+            if (lane == jsel) SC = true;
+            nrem -= 1;
+            if (rem && lane != jsel && rpos == nrem) rpos = at;   // remaining[index] = remaining[--n]
+            if (r4c < 0) sink = jsel;
+            else i = r4c;
+        }
+        if (sink < 0) break;   // unreachable for finite costs
+        // dual update (before augmenting: col4row is the previous matching)
+        const double spc_c = __shfl(spc, col4row < 0 ? 0 : col4row);
+        if (lane == cur) u += minVal;
+        else if (SR) u += minVal - spc_c;
+        if (SC) v -= minVal - spc;
+        // augment along path[] from the sink back to row `cur`
+        int j = sink;
+        for (int guard = 0; guard <= N; ++guard) {
+            const int pi_ = __builtin_amdgcn_readlane(path, j);
+            if (lane == j) row4col = pi_;
+            const int nj = __builtin_amdgcn_readlane(col4row, pi_);
+            if (lane == pi_) col4row = j;
+            j = nj;
+            if (pi_ == cur) break;
+        }
+    }
+    *own = col && col4row >= 0 ? s_cost[lane * N + col4row] : 0.0f;
+    return col ? col4row : -1;
+}
+
+// ---------------------------------------------------------------------------
+// step kernel
+// ---------------------------------------------------------------------------
+__device__ int ragged_env_step(const DevParams &p, const int b, const int lane, unsigned char *lds) {
+    const int Nmax = p.N, Tmax = p.T, Emax = p.E, Mmax = p.M;
+    const int64_t eb = b;
+    float *s_cost = (float *)lds;                               // [N_max][N_max]
+    float2 *s_pos = (float2 *)(lds + 4 * Nmax * Nmax);          // [E] staged rows
+    float2 *pos_b = p.pos + eb * Emax;
+    const bool do_reset = p.mode == kModeReset && (p.env_mask == nullptr || p.env_mask[b] != 0);
+    int t = p.step_count[b];
+    int ep = p.episode[b];
+    float2 acc = p.ep_acc[b];
+    RShape s;
+    float2 cp = make_float2(0.0f, 0.0f), tp = cp, v = cp;   // collider pos, target pos, agent vel
+    bool relaid = false;
+
+    // scenario.reset_world with the Philox layout: compact entity index =
+    // agents, targets, obstacles (a navigation env lays out like the same env
+    // of a navigation batch of N_env agents)
+    auto relayout = [&]() {
+        ep = (p.mode == kModeReset && p.reseed ? -1 : ep) + 1;
+        t = 0;
+        acc = make_float2(0.0f, 0.0f);
+        s = draw_shape(p, b);
+        const uint32_t gid = (uint32_t)(p.env_base + b);
+        cp = make_float2(0.0f, 0.0f);
+        tp = cp;
+        v = cp;
+        if (lane < s.M) cp = layout_at(p, s, gid, (uint32_t)ep, lane < s.N ? lane : s.N + s.T + (lane - s.N));
+        if (lane < s.T) tp = layout_at(p, s, gid, (uint32_t)ep, s.N + lane);
+        relaid = true;
+    };
+    if (do_reset) {
+        relayout();
+    } else {
+        const int32_t sh = p.env_shape[b];
+        s = make_shape(p, sh & 0xFF, sh >> 8);
+        if (lane < s.M) cp = pos_b[collider_row(p, s, lane)];
+        if (lane < s.T) tp = pos_b[Nmax + lane];
+        if (lane < s.N) v = p.vel[eb * Nmax + lane];
+    }
+
+    bool done = false;
+    if (p.mode == kModeStep) {
+        // _set_action + apply_environment_force + integrate_state (App. A S3-S6)
+        float Fx = 0.0f, Fy = 0.0f;
+        if (lane < s.N) {
+            const float2 u = action_force(p, eb * Nmax + lane);
+            Fx = u.x;
+            Fy = u.y;
+        }
+        for (int c = 0; c < s.M; ++c) {
+            const float2 q = rl_f2(cp, c);
+            const float dx = cp.x - q.x, dy = cp.y - q.y;
+            const float d2 = dx * dx + dy * dy;
+            const bool ag = c < s.N;
+            if (lane < s.N && c != lane && d2 > 0.0f && d2 < (ag ? p.cut2_aa : p.cut2_ao)) {
+                const float f = contact_scale(p, d2, ag ? p.dmin_aa : p.dmin_ao);
+                Fx += f * dx;
+                Fy += f * dy;
+            }
+        }
+        if (lane < s.N) {
+            v.x = v.x * p.omd;
+            v.y = v.y * p.omd;
+            v.x = v.x + (Fx / p.mass) * p.dt;
+            v.y = v.y + (Fy / p.mass) * p.dt;
+            if (p.max_speed > 0.0f) {
+                const float sp = sqrtf(v.x * v.x + v.y * v.y);
+                if (sp > p.max_speed) {
+                    v.x = v.x / sp * p.max_speed;
+                    v.y = v.y / sp * p.max_speed;
+                }
+            }
+            cp.x = cp.x + v.x * p.dt;
+            cp.y = cp.y + v.y * p.dt;
+        }
+        t += 1;
+        done = t >= p.EL;
+    }
+
+    // collision cost (agent lanes) and radius row masks (collider lanes)
+    auto pair_sweep = [&](int *cnt) {
+        uint64_t rm = 0;
+        int n = 0;
+        for (int c = 0; c < s.M; ++c) {
+            const float2 q = rl_f2(cp, c);
+            const float dx = cp.x - q.x, dy = cp.y - q.y;
+            const float d2 = dx * dx + dy * dy;
+            const bool other = c != lane;
+            n += (other && d2 < (c < s.N ? p.dmin2_aa : p.dmin2_ao)) ? 1 : 0;
+            rm |= (other && d2 > 0.0f && d2 <= p.R2) ? (1ull << c) : 0ull;
+        }
+        *cnt = n;
+        return lane < s.M ? rm : 0ull;
+    };
+    int cnt = 0;
+    uint64_t rmask = pair_sweep(&cnt);
+    if (lane >= s.N) cnt = 0;
+
+    // reward: navigation -|p_i - g_i|; polygon/line -C[i][sigma_i]
+    float2 slot = make_float2(0.0f, 0.0f);
+    int sigma = -1;
+    float r = 0.0f;
+    if (s.scn == kScnNav) {
+        if (lane < s.N) {
+            const float dx = cp.x - tp.x, dy = cp.y - tp.y;
+            r = -sqrtf(dx * dx + dy * dy);
+        }
+    } else {
+        slot = slot_of(p, s, lane, tp);
+        float own;
+        sigma = wave_lsa(s.N, lane, cp, slot, s_cost, &own);
+        r = -own;
+    }
+    float rsum = wave_sum(lane < s.N ? r : 0.0f);
+    if (p.shared_reward) {
+        r = rsum;
+        rsum *= (float)s.N;
+    }
+    if (lane < Nmax) {
+        p.reward[eb * Nmax + lane] = lane < s.N ? r : 0.0f;
+        p.cost[eb * Nmax + lane] = (float)cnt;
+    }
+    const int csum = wave_sum(cnt);
+
+    if (p.mode == kModeStep) {
+        acc.x += rsum;
+        acc.y += (float)csum;
+        if (done && p.auto_reset) {
+            if (lane == 0) p.ep_last[b] = acc;
+            relayout();
+            // observation of the new layout
+            rmask = pair_sweep(&cnt);
+            if (s.scn != kScnNav) {
+                slot = slot_of(p, s, lane, tp);
+                float own;
+                sigma = wave_lsa(s.N, lane, cp, slot, s_cost, &own);
+            }
+        }
+    }
+
+    // node features [v, p, target - p, type]; target = own goal / assigned slot
+    const bool full = p.mode != kModeStep || relaid;
+    float2 tgt = tp;
+    if (s.scn != kScnNav) {
+        const int src = sigma < 0 ? 0 : sigma;
+        tgt = make_float2(__shfl(slot.x, src), __shfl(slot.y, src));
+    }
+    if (lane < s.N) {
+        float *nf = p.node_feat + (eb * Emax + lane) * 7;
+        nf[0] = v.x;
+        nf[1] = v.y;
+        nf[2] = cp.x;
+        nf[3] = cp.y;
+        nf[4] = tgt.x - cp.x;
+        nf[5] = tgt.y - cp.y;
+        if (full) nf[6] = 0.0f;
+    }
+    if (lane < Nmax) p.assign[eb * Nmax + lane] = (lane < s.N && s.scn != kScnNav) ? sigma : -1;
+
+    if (full) {
+        // every storage row: positions (padding 0) and the static node rows
+        for (int q = lane; q < Emax; q += kWave) s_pos[q] = make_float2(0.0f, 0.0f);
+        wave_sync();
+        if (lane < s.M) s_pos[collider_row(p, s, lane)] = cp;
+        if (lane < s.T) s_pos[Nmax + lane] = tp;
+        wave_sync();
+        for (int q = lane; q < Emax; q += kWave) {
+            const float2 pq = s_pos[q];
+            pos_b[q] = pq;
+            if (q < s.N) continue;   // live agent rows written above
+            float type;
+            if (q < Nmax) type = -1.0f;
+            else if (q < Nmax + Tmax) type = q - Nmax < s.T ? 1.0f : -1.0f;
+            else type = q - Nmax - Tmax < s.O ? 2.0f : -1.0f;
+            float *nf = p.node_feat + (eb * Emax + q) * 7;
+            nf[0] = 0.0f;
+            nf[1] = 0.0f;
+            nf[2] = pq.x;
+            nf[3] = pq.y;
+            nf[4] = 0.0f;
+            nf[5] = 0.0f;
+            nf[6] = type;
+        }
+        if (lane < Nmax) p.vel[eb * Nmax + lane] = lane < s.N ? v : make_float2(0.0f, 0.0f);
+    } else if (lane < s.N) {
+        pos_b[lane] = cp;
+        p.vel[eb * Nmax + lane] = v;
+    }
+
+    if (lane < s.M) p.row_mask[eb * Mmax + lane] = rmask;
+    const int edges = wave_sum((int)__popcll(rmask)) + 2 * s.N * s.Tper;
+    if (lane == 0) {
+        p.step_count[b] = t;
+        p.episode[b] = ep;
+        p.ep_acc[b] = acc;
+        p.done[b] = done ? 1 : 0;
+        p.edge_count[b] = edges;
+        if (relaid) p.env_shape[b] = s.N | (s.scn << 8);
+    }
+    return edges;
+}
+
+__global__ __launch_bounds__(kBlock) void gsm_step_ragged_kernel(DevParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int b = blockIdx.x * kWavesPerBlock + wave;
+    int edges = 0;
+    if (b < p.B) edges = ragged_env_step(p, b, lane, smem + wave * p.wave_lds_step);
+    int *s_bc = (int *)(smem + kWavesPerBlock * p.wave_lds_step);
+    if (lane == 0) s_bc[wave] = edges;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int sum = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) sum += s_bc[w];
+        p.block_edge_sum[blockIdx.x] = sum;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// edge emitter
+// ---------------------------------------------------------------------------
+__device__ void ragged_env_emit(const DevParams &p, const int b, const int lane, const int64_t off,
+                                unsigned char *lds) {
+    const int Nmax = p.N, Tmax = p.T, Emax = p.E, Mmax = p.M;
+    const int64_t eb = b;
+    float2 *s_pos = (float2 *)lds;
+    const int32_t sh = p.env_shape[b];
+    const RShape s = make_shape(p, sh & 0xFF, sh >> 8);
+    for (int q = lane; q < Emax; q += kWave) s_pos[q] = p.pos[eb * Emax + q];
+    wave_sync();
+    int32_t *const src = p.edge_index;
+    int32_t *const dst = p.edge_index + p.edge_capacity;
+    const int32_t g0 = (int32_t)(eb * Emax);
+    const uint64_t mask = lane < s.M ? p.row_mask[eb * Mmax + lane] : 0ull;
+    const int cnt = __popcll(mask) + (lane < s.N ? s.Tper : 0);
+    const int incl = wave_scan(cnt);
+    const int agent_total = s.N > 0 ? __builtin_amdgcn_readlane(incl, s.N - 1) : 0;
+    // row order: agent rows, target rows (N*Tper edges), obstacle rows
+    int64_t o = off + (incl - cnt) + (lane >= s.N ? s.N * s.Tper : 0);
+    auto put = [&](int a_row, float2 a, int d_row) {
+        const float2 q = s_pos[d_row];
+        const float dx = a.x - q.x, dy = a.y - q.y;
+        src[o] = g0 + a_row;
+        dst[o] = g0 + d_row;
+        p.edge_attr[o] = sqrtf(dx * dx + dy * dy);
+        ++o;
+    };
+    if (lane < s.M) {
+        const int row = collider_row(p, s, lane);
+        const float2 a = s_pos[row];
+        const uint64_t amask = s.N >= 64 ? ~0ull : ((1ull << s.N) - 1ull);
+        uint64_t am = mask & amask, om = mask & ~amask;
+        while (am) {
+            const int c = __builtin_ctzll(am);
+            am &= am - 1;
+            put(row, a, c);
+        }
+        if (lane < s.N) {
+            if (s.scn == kScnNav) {
+                put(row, a, Nmax + lane);
+            } else {
+                put(row, a, Nmax);
+                if (s.Tper == 2) put(row, a, Nmax + 1);
+            }
+        }
+        while (om) {
+            const int c = __builtin_ctzll(om);
+            om &= om - 1;
+            put(row, a, Nmax + Tmax + (c - s.N));
+        }
+    }
+    // target rows: goal i -> agent i; centre / line ends -> every agent
+    if (lane < s.N) {
+        const int64_t tb = off + agent_total;
+        if (s.scn == kScnNav) {
+            o = tb + lane;
+            put(Nmax + lane, s_pos[Nmax + lane], lane);
+        } else {
+            o = tb + lane;
+            put(Nmax, s_pos[Nmax], lane);
+            if (s.Tper == 2) {
+                o = tb + s.N + lane;
+                put(Nmax + 1, s_pos[Nmax + 1], lane);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void gsm_emit_ragged_kernel(DevParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    int *s_red = (int *)(smem + kWavesPerBlock * p.wave_lds_emit);
+    // exclusive prefix of the step kernel's per-workgroup edge sums
+    int acc = 0;
+    for (int k = threadIdx.x; k < (int)blockIdx.x; k += kBlock) acc += p.block_edge_sum[k];
+    acc = wave_sum(acc);
+    if (lane == 0) s_red[wave] = acc;
+    __syncthreads();
+    int64_t off = 0;
+    for (int w = 0; w < kWavesPerBlock; ++w) off += s_red[w];
+    const int b0 = blockIdx.x * kWavesPerBlock;
+    for (int w = 0; w < wave && b0 + w < p.B; ++w) off += p.edge_count[b0 + w];
+    const int b = b0 + wave;
+    if (b >= p.B) return;
+    if (lane == 0) {
+        p.edge_ptr[b] = off;
+        if (b == p.B - 1) p.edge_ptr[p.B] = off + p.edge_count[b];
+    }
+    ragged_env_emit(p, b, lane, off, smem + wave * p.wave_lds_emit);
+}
+
+const void *step_ragged_kernel_fn() { return reinterpret_cast<const void *>(&gsm_step_ragged_kernel); }
+const void *emit_ragged_kernel_fn() { return reinterpret_cast<const void *>(&gsm_emit_ragged_kernel); }
+
+// Host side: the tables come from float64 libm and are rounded to fp32 once,
+// exactly as oracle/ragged_ref.py forms them (math.cos/sin/sqrt, same
+// operation order), so slots and half-widths agree bit for bit.
+hipError_t upload_ragged_tables() {
+    static std::mutex mu;
+    static bool done[256] = {};
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lock(mu);
+    if (dev >= 0 && dev < 256 && done[dev]) return hipSuccess;
+    std::vector<float2> unit(kRaggedTable);
+    std::vector<float> lt(kRaggedTable);
+    float hw[kRaggedMaxAgents + 1];
+    hw[0] = 0.0f;
+    for (int n = 1; n <= kRaggedMaxAgents; ++n) {
+        hw[n] = (float)sqrt(n / 3.0);
+        for (int j = 0; j < n; ++j) {
+            const double a = 2.0 * M_PI * j / n;
+            unit[tri(n) + j] = make_float2((float)cos(a), (float)sin(a));
+            lt[tri(n) + j] = n == 1 ? 0.5f : (float)((double)j / (double)(n - 1));
+        }
+    }
+    e = hipMemcpyToSymbol(HIP_SYMBOL(c_unit), unit.data(), sizeof(float2) * kRaggedTable);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(c_linet), lt.data(), sizeof(float) * kRaggedTable);
+    if (e == hipSuccess) e = hipMemcpyToSymbol(HIP_SYMBOL(c_halfw), hw, sizeof hw);
+    if (e == hipSuccess && dev >= 0 && dev < 256) done[dev] = true;
+    return e;
+}
+
+}  // namespace gsm

@@ -11,7 +11,7 @@ import os
 from pathlib import Path
 
 LIB_PATH = Path(os.environ.get("GSM_LIB_PATH") or Path(__file__).resolve().parent / "lib" / "libgsm.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 GSM_OK, GSM_EINVAL, GSM_EHIP, GSM_ESTATE = 0, -1, -2, -3
 GRAPH_SLOTS = 4
@@ -30,6 +30,7 @@ class GsmConfig(C.Structure):
         ("max_speed", C.c_float), ("world_half", C.c_float),
         ("agent_size", C.c_float), ("goal_size", C.c_float), ("obstacle_size", C.c_float),
         ("sense_radius", C.c_float), ("contact_cutoff", C.c_float),
+        ("n_agents_min", C.c_int32), ("formation_radius", C.c_float),
     ]
 
 
@@ -37,13 +38,13 @@ class GsmSizes(C.Structure):
     _fields_ = [
         ("n_entities", C.c_int32), ("node_feat_dim", C.c_int32), ("obs_dim", C.c_int32),
         ("envs_per_block", C.c_int32), ("n_blocks", C.c_int32), ("max_edges_per_env", C.c_int32),
-        ("edge_capacity", C.c_int64),
+        ("edge_capacity", C.c_int64), ("n_colliders", C.c_int32), ("n_targets", C.c_int32),
     ]
 
 
 BUFFER_FIELDS = ["pos", "vel", "step_count", "episode", "ep_acc", "ep_last", "node_feat",
                  "reward", "cost", "done", "edge_count", "block_edge_sum", "edge_ptr",
-                 "edge_index", "edge_attr", "row_mask", "contact_mask"]
+                 "edge_index", "edge_attr", "row_mask", "contact_mask", "env_shape", "assign"]
 
 
 class GsmBuffers(C.Structure):
@@ -118,8 +119,9 @@ def make_config(cfg) -> GsmConfig:
     c.env_base, c.seed = int(cfg.env_base), int(cfg.seed) & 0xFFFFFFFFFFFFFFFF
     for f in ("dt", "damping", "mass", "contact_force", "contact_margin", "sensitivity",
               "max_speed", "world_half", "agent_size", "goal_size", "obstacle_size",
-              "sense_radius", "contact_cutoff"):
+              "sense_radius", "contact_cutoff", "formation_radius"):
         setattr(c, f, float(getattr(cfg, f)))
+    c.n_agents_min = int(cfg.n_agents_min)
     return c
 
 

@@ -67,8 +67,11 @@ class GpuBatchEnv:
             edge_index=torch.zeros(2, cap, dtype=i32, device=dev),
             edge_attr=torch.zeros(cap, dtype=f32, device=dev),
             # derived state (refreshed by every reset/step/observe)
-            row_mask=torch.zeros(B, N + cfg.n_obstacles, dtype=torch.int64, device=dev),
+            row_mask=torch.zeros(B, self.sizes.n_colliders, dtype=torch.int64, device=dev),
             contact_mask=torch.zeros(B, N, dtype=torch.int64, device=dev),
+            # ragged batches: N_env | scenario << 8, and the LSA slot of each agent
+            env_shape=torch.zeros(B, dtype=i32, device=dev),
+            assign=torch.full((B, N), -1, dtype=i32, device=dev),
         )
         bufs = _lib.GsmBuffers(**{k: self.t[k].data_ptr() for k in _lib.BUFFER_FIELDS})
         _lib.check(self.lib, self.lib.gsm_bind(self._h, C.byref(bufs)), self._h, "gsm_bind")
@@ -99,6 +102,10 @@ class GpuBatchEnv:
         out = dict(obs=t["node_feat"][:, : self.N, :6], node_feat=t["node_feat"],
                    agent_id=self.agent_id, reward=t["reward"], cost=t["cost"], done=t["done"],
                    edge_ptr=t["edge_ptr"])
+        if self.cfg.ragged:
+            out["assign"] = t["assign"]
+            out["n_agents_env"] = t["env_shape"] & 0xFF
+            out["scenario_env"] = t["env_shape"] >> 8
         if sync_edges:
             total = int(t["edge_ptr"][self.B].item())
             out["edge_index"] = t["edge_index"][:, :total]

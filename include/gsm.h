@@ -32,7 +32,7 @@
 extern "C" {
 #endif
 
-#define GSM_ABI_VERSION 2
+#define GSM_ABI_VERSION 3
 
 typedef enum gsm_status {
     GSM_OK = 0,
@@ -42,8 +42,17 @@ typedef enum gsm_status {
 } gsm_status;
 
 typedef enum gsm_scenario {
-    GSM_SCEN_NAVIGATION = 0,   /* scenarios/exp1.py|exp2.py (SOURCES.txt:21-22) */
+    GSM_SCEN_NAVIGATION = 0,   /* scenarios/exp1.py|exp2.py (SOURCES.txt:21-22)          */
+    GSM_SCEN_POLYGON = 1,      /* scenarios/simple_formation.py (SOURCES.txt:24; readme.md:89) */
+    GSM_SCEN_LINE = 2,         /* scenarios/simple_line.py (SOURCES.txt:25; readme.md:90)      */
+    GSM_SCEN_MIXED = 3,        /* env id mod 3 -> navigation/polygon/line, N per env drawn   */
 } gsm_scenario;
+
+/* Ragged batches (polygon, line, mixed): every env has its own agent count
+ * N_env <= n_agents (= N_max <= GSM_RAGGED_MAX_AGENTS) and its own scenario,
+ * stored padded: entity rows agents [0, N_max), targets [N_max, N_max+T_max),
+ * obstacles [N_max+T_max, E). env_shape[b] = N_env | scenario << 8. */
+#define GSM_RAGGED_MAX_AGENTS 32
 
 typedef enum gsm_action_fmt {
     GSM_ACT_ONEHOT = 0,   /* float32 [B][N][5]; u = [a1-a2, a3-a4] (MPE discrete_action_space) */
@@ -78,6 +87,9 @@ typedef struct gsm_config {
     float agent_size, goal_size, obstacle_size;
     float sense_radius;       /* R: graph edge radius                        */
     float contact_cutoff;     /* skip pair force when d - dmin > cutoff*k     */
+    /* ragged scenarios (ignored by navigation) */
+    int32_t n_agents_min;     /* mixed: N_env drawn from [n_agents_min, n_agents] */
+    float formation_radius;   /* polygon: N-gon radius (readme.md:89 -> 0.5)  */
 } gsm_config;
 
 /* Sizes the caller must allocate (gsm_query_sizes). */
@@ -89,12 +101,14 @@ typedef struct gsm_sizes {
     int32_t n_blocks;         /* length of block_edge_sum                    */
     int32_t max_edges_per_env;
     int64_t edge_capacity;    /* length of edge_attr and of each edge_index row */
+    int32_t n_colliders;      /* M = row_mask entries per env (agents + obstacles) */
+    int32_t n_targets;        /* T_max: goal/landmark rows per env            */
 } gsm_sizes;
 
 /* Caller-owned device buffers (all contiguous, row-major). */
 typedef struct gsm_buffers {
     /* state */
-    float *pos;               /* [B][E][2]   agents, goals, obstacles         */
+    float *pos;               /* [B][E][2]   agents, goals/landmarks, obstacles */
     float *vel;               /* [B][N][2]   agents only (landmarks immovable) */
     int32_t *step_count;      /* [B]         steps since reset                */
     int32_t *episode;         /* [B]         episode index (-1 before reset)  */
@@ -112,8 +126,11 @@ typedef struct gsm_buffers {
     float *edge_attr;         /* [edge_capacity]    distance                  */
     /* derived state, valid for the positions in `pos` after any reset/step/
      * observe; a caller that rewrites `pos`/`vel` must call gsm_observe      */
-    uint64_t *row_mask;       /* [B][N+No] radius adjacency rows (bit = collider) */
-    uint64_t *contact_mask;   /* [B][N]    contact candidates of each agent        */
+    uint64_t *row_mask;       /* [B][M] radius adjacency rows (bit = collider) */
+    uint64_t *contact_mask;   /* [B][N] contact candidates of each agent        */
+    /* ragged scenarios only (may be NULL for navigation) */
+    int32_t *env_shape;       /* [B]    N_env | scenario << 8 (set at every layout) */
+    int32_t *assign;          /* [B][N] polygon/line slot of each agent (LSA), -1 else */
 } gsm_buffers;
 
 typedef struct gsm_handle gsm_handle;
