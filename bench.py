@@ -47,27 +47,32 @@ def step_kernel_bytes(B, N, No, EL, action_bytes, seg=True):
     node-feature rows (goal/obstacle rows are static within an episode), reward,
     cost, the new masks, counters, done, edge count and the per-block edge sum.
     Re-layout at episode end rewrites goal/obstacle pos and static node rows:
-    amortised over the episode length. Generic path (M > 64): no masks, every
-    node-feature row written each step."""
+    amortised over the episode length. Tile path (M > 64): the same with
+    W = ceil(M/64) mask words per row; obstacle rows re-read their
+    obstacle-only words and rewrite the chunks holding agent columns; agent
+    node-feature rows are 6 floats per step (the type column is static)."""
     E, M = 2 * N + No, N + No
     if seg:
         reads = 8 * E + 8 * N + action_bytes * N + 16 + 8 * N + 8 * No
         writes = 8 * N + 8 * N + 28 * N + 4 * N + 4 * N + 8 * N + 8 * M + 16 + 1 + 4
         reset = (8 * (E - N) + 28 * (E - N) + 8) / EL
+        per_block = 4 * min(64 // M, 16)
     else:
-        reads = 8 * E + 8 * N + action_bytes * N + 16
-        writes = 8 * N + 8 * N + 28 * E + 4 * N + 4 * N + 16 + 1 + 4
-        reset = (8 * (E - N) + 8) / EL
-    envs_per_block = 4 * (min(64 // M, 16) if seg else 1)
-    return B * (reads + writes + reset + 4 / envs_per_block)
+        W, ka = (M + 63) // 64, (N + 63) // 64
+        reads = 8 * E + 8 * N + action_bytes * N + 16 + 8 * N * W + 8 * No * (W - ka)
+        writes = 8 * N + 8 * N + 24 * N + 4 * N + 4 * N + 8 * N * W + 8 * (N * W + No * ka) + 16 + 1 + 4
+        reset = (8 * (E - N) + 28 * (E - N) + 4 * N + 8) / EL
+        per_block = 1
+    return B * (reads + writes + reset + 4 / per_block)
 
 
 def emit_kernel_bytes(B, N, No, total_edges, seg=True):
-    """Algorithmic HBM bytes of one edge-emit launch: entity positions (and
-    the adjacency row masks on the segmented path), the env's edge count, the
-    int64 edge_ptr entry and 12 B per edge (src, dst int32 + fp32 distance)."""
+    """Algorithmic HBM bytes of one edge-emit launch: entity positions, the
+    adjacency row masks (W = ceil(M/64) words per collider row on the tile
+    path, 1 on the segmented path), the env's edge count, the int64 edge_ptr
+    entry and 12 B per edge (src, dst int32 + fp32 distance)."""
     E, M = 2 * N + No, N + No
-    per_env = 8 * E + 4 + 8 + (8 * M if seg else 0)
+    per_env = 8 * E + 4 + 8 + 8 * M * (1 if seg else (M + 63) // 64)
     return B * per_env + 12 * total_edges
 
 
@@ -289,8 +294,8 @@ def main():
         else:
             sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4, seg)
             eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)
-            names = ("gsm_step_seg_kernel", "gsm_emit_seg_kernel") if seg else ("gsm_step_kernel",
-                                                                               "gsm_emit_edges_kernel")
+            names = ("gsm_step_seg_kernel", "gsm_emit_seg_kernel") if seg else ("gsm_step_tile_kernel",
+                                                                               "gsm_emit_tile_kernel")
         kern = {"step": dict(kernel=names[0], ms=step_ms, bytes=sb, gbs=sb / (step_ms * 1e-3) / 1e9),
                 "emit": dict(kernel=names[1], ms=emit_ms, bytes=eb, gbs=eb / (emit_ms * 1e-3) / 1e9)}
         dom = "step" if step_ms >= emit_ms else "emit"

@@ -112,7 +112,7 @@ void choose_path(const gsm_config *c, int *path, int *G) {
         int g = gsm::kWave / M;
         *G = g > gsm::kMaxSegEnvsPerWave ? gsm::kMaxSegEnvsPerWave : g;
     } else {
-        *path = gsm::kPathGeneric;
+        *path = gsm::kPathTile;
         *G = 1;
     }
 }
@@ -134,7 +134,7 @@ void fill_sizes(const gsm_config *c, gsm_sizes *s) {
     s->n_entities = N + T + No;
     s->node_feat_dim = 7;
     s->obs_dim = 6;
-    s->envs_per_block = gsm::kWavesPerBlock * G;
+    s->envs_per_block = path == gsm::kPathTile ? 1 : gsm::kWavesPerBlock * G;
     s->n_blocks = (c->n_envs + s->envs_per_block - 1) / s->envs_per_block;
     // radius edges among colliders + the agent <-> target edges (2 per agent
     // per target it is tied to: own goal / centre: 1, line ends: 2)
@@ -144,6 +144,7 @@ void fill_sizes(const gsm_config *c, gsm_sizes *s) {
     s->max_edges_per_env = max_edges;
     s->n_colliders = M;
     s->n_targets = T;
+    s->mask_words = path == gsm::kPathTile ? (M + 63) / 64 : 1;
     s->edge_capacity = (int64_t)c->n_envs * s->max_edges_per_env;
 }
 
@@ -160,11 +161,7 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
     p->scenario = c->scenario;
     p->n_min = c->scenario == GSM_SCEN_MIXED ? c->n_agents_min : N;
     choose_path(c, &p->path, &p->G);
-    // generic path: N*S lanes of the wave share the contact loop
-    int S = N <= gsm::kWave ? gsm::kWave / N : 1;
-    if (S > p->M) S = p->M;
-    if (S < 1) S = 1;
-    p->S = S;
+    p->W = p->path == gsm::kPathTile ? (p->M + 63) / 64 : 1;
     p->EL = c->episode_length;
     p->auto_reset = c->auto_reset != 0;
     p->shared_reward = c->shared_reward != 0;
@@ -180,8 +177,9 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
         p->wave_lds_step = align16(8 * p->G * p->E + 28 * p->G * p->E);
         p->wave_lds_emit = align16(8 * p->G * p->E);
     } else {
-        p->wave_lds_step = align16(8 * p->E + 8 * N + 12 * S * N);
-        p->wave_lds_emit = align16(8 * p->E);
+        // tile: whole-workgroup LDS: positions, velocities, new positions, costs, reductions
+        p->wave_lds_step = align16(8 * p->E + 8 * N + 8 * N + 4 * N + 8 * (gsm::kTileBlock / gsm::kWave));
+        p->wave_lds_emit = align16(8 * p->E + 4 * (gsm::kTileBlock / gsm::kWave));
     }
     const float L = c->world_half;
     p->L = L;
@@ -401,7 +399,7 @@ int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t 
         void *args[] = {&p};
         kp.func = const_cast<void *>(fn);
         kp.gridDim = dim3(gsm::grid_blocks(p));
-        kp.blockDim = dim3(gsm::kBlock);
+        kp.blockDim = dim3(gsm::block_threads(p));
         kp.sharedMemBytes = (unsigned)lds;
         kp.kernelParams = args;
         kp.extra = nullptr;

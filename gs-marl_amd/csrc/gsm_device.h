@@ -1,4 +1,4 @@
-// Device helpers shared by the generic and the segmented kernel families.
+// Device helpers shared by the segmented, tile and ragged kernel families.
 #pragma once
 #include "gsm_internal.h"
 #include "gsm_philox.h"

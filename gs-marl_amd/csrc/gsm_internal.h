@@ -8,7 +8,11 @@ namespace gsm {
 constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;              // one env per wave
 constexpr int kBlock = kWave * kWavesPerBlock;
-enum : int32_t { kPathGeneric = 0, kPathSeg = 1, kPathRagged = 2 };
+enum : int32_t { kPathSeg = 1, kPathRagged = 2, kPathTile = 3 };
+#ifndef GSM_TILE_BLOCK
+#define GSM_TILE_BLOCK 512
+#endif
+constexpr int kTileBlock = GSM_TILE_BLOCK;     // tile path: one workgroup per env
 enum : int32_t { kScnNav = 0, kScnPolygon = 1, kScnLine = 2, kScnMixed = 3 };
 constexpr int kRaggedMaxAgents = 32;                                  // = GSM_RAGGED_MAX_AGENTS
 constexpr int kRaggedTable = kRaggedMaxAgents * (kRaggedMaxAgents + 1) / 2;   // rows n = 1..32
@@ -18,12 +22,13 @@ constexpr int kMaxSegEnvsPerWave = 16;   // keeps a block's envs (4G) within one
 // fp32 constants are formed on the host exactly as oracle/batch_ref.py:Spec
 // forms them in fp32 mode (gsm_abi.hip: derive()).
 struct DevParams {
-    int32_t B, N, No, E, M, S, EL, auto_reset, shared_reward;
+    int32_t B, N, No, E, M, EL, auto_reset, shared_reward;
     int32_t mode, action_fmt, reseed;
-    int32_t path;          // kPathSeg (M <= 64), kPathGeneric or kPathRagged
+    int32_t path;          // kPathSeg (navigation, M <= 64), kPathTile (M > 64) or kPathRagged
     int32_t scenario;      // ragged: kScnPolygon / kScnLine / kScnMixed
     int32_t T;             // ragged: target rows per env (T_max); N, No, E, M are the padded maxima
     int32_t n_min;         // ragged mixed: smallest N_env
+    int32_t W;             // uint64 words per mask row (tile path: ceil(M/64))
     int32_t G;             // envs per wave (segmented path), 1 otherwise
     uint32_t seed_lo, seed_hi;
     int64_t env_base;
@@ -62,6 +67,9 @@ const void *emit_kernel_fn(const DevParams &p);
 const void *step_seg_kernel_fn(const DevParams &p);
 const void *emit_seg_kernel_fn(const DevParams &p);
 const void *step_ragged_kernel_fn();
+const void *step_tile_kernel_fn();
+const void *emit_tile_kernel_fn();
+int block_threads(const DevParams &p);
 const void *emit_ragged_kernel_fn();
 // ragged path: per-device constant tables (unit circle, line fractions,
 // half-widths) computed on the host with libm; uploaded once per device.

@@ -1,0 +1,458 @@
+// gsm_tile_kernels.hip — navigation envs with more than 64 colliders
+// (BASELINE config C3: 96 agents, 96 obstacles -> 192 colliders, 288 entities).
+//
+// One 512-thread workgroup (8 waves) per env: a wave per env would leave one
+// wave per SIMD at C3 (1024 envs on 1024 SIMDs) with nothing to hide the
+// O(M^2) pair loops' latency. Entity positions live in LDS; the work is split
+// over the workgroup:
+//
+//  gsm_step_tile_kernel  force pass over the contact candidates recorded by
+//                        the previous step's sweep (sparse: pairs within the
+//                        contact cutoff), integrate, then one sweep over all
+//                        collider rows (wave w: rows w, w+8, ...; lanes =
+//                        64-collider chunks) ballots the radius adjacency,
+//                        the next contact candidates and the collisions into
+//                        mask words (row_mask / contact_mask, W = ceil(M/64)
+//                        words per row). Node features: agent rows every
+//                        step, static rows on layout change.
+//  gsm_emit_tile_kernel  thread = a contiguous run of rows; counts from the
+//                        mask popcounts, a workgroup scan, then each thread
+//                        walks its rows' set bits and writes the row-major
+//                        COO edges with their distances.
+//
+// Same arithmetic contract as the other paths (d2 = dx*dx + dy*dy without
+// contraction, squared predicates).
+#include "gsm_device.h"
+
+namespace gsm {
+
+constexpr int kTileWaves = kTileBlock / kWave;
+
+// workgroup sums (every thread gets the total); s_red holds kTileWaves slots
+__device__ __forceinline__ int tile_sum(int v, int *s_red) {
+    const int wave = threadIdx.x >> 6;
+    v = wave_total(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_red[wave] = v;
+    __syncthreads();
+    int t = 0;
+#pragma unroll
+    for (int w = 0; w < kTileWaves; ++w) t += s_red[w];
+    return t;
+}
+__device__ __forceinline__ float tile_sum(float v, float *s_red) {
+    const int wave = threadIdx.x >> 6;
+    v = wave_total(v);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) s_red[wave] = v;
+    __syncthreads();
+    float t = 0.0f;
+#pragma unroll
+    for (int w = 0; w < kTileWaves; ++w) t += s_red[w];
+    return t;
+}
+
+// Post-step sweep over every collider row r (wave w takes rows w, w+8, ...):
+// lane l of chunk k holds collider c = 64k + l; one ballot per (row, chunk)
+// and predicate yields the row's words of
+//   rad     c != r, 0 < d2 <= R^2           -> row_mask  [B][M][W]
+//   contact c != r, 0 < d2 < cut^2 (agents) -> contact_mask [B][N][W]
+//            (the next step's force pass visits only these pairs: its
+//             pre-step positions are exactly these post-step positions)
+//   collide c != r, d2 < dmin^2 (agents)    -> cost (popcount)
+// Row positions are held one per lane and broadcast with v_readlane (no LDS
+// in the inner loop); words are gathered into lane j (the wave's j-th row of
+// the group) with v_writelane and stored by that lane. Obstacle rows keep
+// their obstacle-only words (static within an episode) when `keep_oo`.
+// Returns this thread's share of the directed radius pair count and leaves
+// agent collision counts in s_cost.
+template <int kW>   // mask words per row; 0 = runtime p.W
+__device__ __forceinline__ int obs_sweep(const DevParams &p, const float2 *s_pos, int *s_cost, int64_t eb,
+                                         bool keep_oo) {
+    const int N = p.N, M = p.M, W = kW > 0 ? kW : p.W;
+    constexpr int kR = kW > 0 ? kW : 1;     // words held in registers per pass
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int rows_w = (M - wave + kTileWaves - 1) / kTileWaves;   // rows r = wave + 8j
+    const int arows_w = N > wave ? (N - wave + kTileWaves - 1) / kTileWaves : 0;   // agent rows first
+    uint64_t *const rmask = p.row_mask + eb * M * W;
+    uint64_t *const cmask = p.contact_mask + eb * N * W;
+    // obstacle rows recompute only the chunks holding agent columns when the
+    // obstacle-only words are still valid (same layout as the last sweep)
+    const int kc_obst = keep_oo ? (N + 63) / 64 : W;
+    // t = bits(d2) - 1:  0 < d2 <= R^2 <=> t <u bits(R^2);  0 < d2 < cut^2 <=>
+    // t <u bits(cut^2) - 1 (d2 is never negative). Both exclude the row's own
+    // column (d2 = 0) by themselves; lanes past M hold an infinite position.
+    const uint32_t R2b = (uint32_t)__float_as_int(p.R2);
+    int pairs = 0;   // per lane: set bits of the words it stores / keeps
+    for (int g0 = 0; g0 < rows_w; g0 += kWave) {
+        const int ng = min(kWave, rows_w - g0);
+        const int ja = min(ng, max(0, arows_w - g0));   // rows [0, ja) of the group are agent rows
+        const int rl = wave + kTileWaves * (g0 + lane);
+        const float2 rowp = lane < ng ? s_pos[collider_entity(rl, N)] : make_float2(0.0f, 0.0f);
+        uint32_t cnt = 0;   // lane j: collisions of its row (own column included)
+        for (int k0 = 0; k0 < W; k0 += kR) {
+            float2 q[kR];
+            float dmin2[kR];
+            uint32_t cutb[kR];
+            uint32_t rad_lo[kR], rad_hi[kR], con_lo[kR], con_hi[kR];
+#pragma unroll
+            for (int u = 0; u < kR; ++u) {
+                const int c = 64 * (k0 + u) + lane;
+                q[u] = c < M ? s_pos[collider_entity(c, N)] : make_float2(__builtin_inff(), __builtin_inff());
+                dmin2[u] = c < N ? p.dmin2_aa : p.dmin2_ao;
+                cutb[u] = (uint32_t)__float_as_int(c < N ? p.cut2_aa : p.cut2_ao) - 1u;
+                con_lo[u] = con_hi[u] = 0;
+                uint64_t old = 0;
+                if (k0 + u >= kc_obst && k0 + u < W && lane >= ja && lane < ng)
+                    old = rmask[(int64_t)rl * W + k0 + u];   // obstacle-only word: unchanged
+                rad_lo[u] = (uint32_t)old;
+                rad_hi[u] = (uint32_t)(old >> 32);
+            }
+            for (int j = 0; j < ja; ++j) {   // agent rows: radius, contact, collision
+                const float ax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rowp.x), j));
+                const float ay = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rowp.y), j));
+                uint32_t ncol = 0;
+#pragma unroll
+                for (int u = 0; u < kR; ++u) {
+                    if (kW == 0 && k0 + u >= W) break;
+                    const float dx = ax - q[u].x, dy = ay - q[u].y;
+                    const float d2 = dx * dx + dy * dy;
+                    const uint32_t tb = (uint32_t)__float_as_int(d2) - 1u;
+                    const uint64_t rad = __builtin_amdgcn_ballot_w64(tb < R2b);
+                    const uint64_t con = __builtin_amdgcn_ballot_w64(tb < cutb[u]);
+                    ncol += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(d2 < dmin2[u]));
+                    rad_lo[u] = writelane_u32((uint32_t)rad, (uint32_t)j, rad_lo[u]);
+                    rad_hi[u] = writelane_u32((uint32_t)(rad >> 32), (uint32_t)j, rad_hi[u]);
+                    con_lo[u] = writelane_u32((uint32_t)con, (uint32_t)j, con_lo[u]);
+                    con_hi[u] = writelane_u32((uint32_t)(con >> 32), (uint32_t)j, con_hi[u]);
+                }
+                cnt = writelane_u32(__builtin_amdgcn_readlane(cnt, j) + ncol, (uint32_t)j, cnt);
+            }
+            const int kc = min(kR, kc_obst - k0);   // chunks computed for obstacle rows
+            for (int j = ja; j < ng; ++j) {  // obstacle rows: radius only
+                const float ax = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rowp.x), j));
+                const float ay = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(rowp.y), j));
+#pragma unroll
+                for (int u = 0; u < kR; ++u) {
+                    if (u >= kc) break;
+                    const float dx = ax - q[u].x, dy = ay - q[u].y;
+                    const float d2 = dx * dx + dy * dy;
+                    const uint32_t tb = (uint32_t)__float_as_int(d2) - 1u;
+                    const uint64_t rad = __builtin_amdgcn_ballot_w64(tb < R2b);
+                    rad_lo[u] = writelane_u32((uint32_t)rad, (uint32_t)j, rad_lo[u]);
+                    rad_hi[u] = writelane_u32((uint32_t)(rad >> 32), (uint32_t)j, rad_hi[u]);
+                }
+            }
+            if (lane < ng) {
+#pragma unroll
+                for (int u = 0; u < kR; ++u) {
+                    const int k = k0 + u;
+                    if (kW == 0 && k >= W) break;
+                    pairs += __popc(rad_lo[u]) + __popc(rad_hi[u]);
+                    if (lane >= ja && k >= kc_obst) continue;   // kept word: already stored
+                    rmask[(int64_t)rl * W + k] = ((uint64_t)rad_hi[u] << 32) | rad_lo[u];
+                    if (lane < ja) cmask[(int64_t)rl * W + k] = ((uint64_t)con_hi[u] << 32) | con_lo[u];
+                }
+            }
+        }
+        if (lane < ja) s_cost[rl] = (int)cnt - 1;   // minus the row's own column
+    }
+    return pairs;
+}
+
+__device__ __forceinline__ int obs_sweep_any(const DevParams &p, const float2 *s_pos, int *s_cost, int64_t eb,
+                                             bool keep_oo) {
+    switch (p.W) {
+        case 2: return obs_sweep<2>(p, s_pos, s_cost, eb, keep_oo);
+        case 3: return obs_sweep<3>(p, s_pos, s_cost, eb, keep_oo);
+        case 4: return obs_sweep<4>(p, s_pos, s_cost, eb, keep_oo);
+        default: return obs_sweep<0>(p, s_pos, s_cost, eb, keep_oo);
+    }
+}
+
+#ifdef GSM_TILE_OCC8   // experiment: force 8 waves/SIMD (spills registers)
+#define GSM_TILE_ATTR __attribute__((amdgpu_waves_per_eu(8)))
+#else
+#define GSM_TILE_ATTR
+#endif
+__global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel(DevParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x;
+    const int N = p.N, E = p.E, W = p.W;
+    float2 *s_pos = (float2 *)smem;           // [E]
+    float2 *s_vel = s_pos + E;                // [N]
+    float2 *s_np = s_vel + N;                 // [N] integrated agent positions
+    int *s_cost = (int *)(s_np + N);          // [N]
+    int *s_ired = s_cost + N;                 // [kTileWaves]
+    float *s_fred = (float *)(s_ired + kTileWaves);
+    const int64_t eb = b;
+
+    // Issue every global read of the step up front (positions, velocities,
+    // this thread's agent action and contact-candidate words) so their
+    // latencies overlap instead of chaining through the phases below.
+    constexpr int kPre = 4;   // contact words prefetched per agent (W <= 4)
+    const bool step_mode = p.mode == kModeStep;
+    uint64_t cw[kPre] = {0, 0, 0, 0};
+    float2 u0 = make_float2(0.0f, 0.0f);
+    if (step_mode && tid < N) {
+        u0 = action_force(p, eb * N + tid);
+        const uint64_t *cm = p.contact_mask + (eb * N + tid) * W;
+#pragma unroll
+        for (int k = 0; k < kPre; ++k)
+            if (k < W) cw[k] = cm[k];
+    }
+    for (int e = tid; e < E; e += kTileBlock) s_pos[e] = p.pos[eb * E + e];
+    for (int i = tid; i < N; i += kTileBlock) s_vel[i] = p.vel[eb * N + i];
+    int t = p.step_count[b];
+    int ep = p.episode[b];
+    float2 acc = p.ep_acc[b];
+    const bool do_reset = p.mode == kModeReset && (p.env_mask == nullptr || p.env_mask[b] != 0);
+    bool relaid = false;
+    __syncthreads();
+
+    auto relayout = [&]() {   // scenario.reset_world with the Philox layout
+        ep = (p.mode == kModeReset && p.reseed ? -1 : ep) + 1;
+        t = 0;
+        acc = make_float2(0.0f, 0.0f);
+        const uint32_t gid = (uint32_t)(p.env_base + b);
+        __syncthreads();
+        for (int e = tid; e < E; e += kTileBlock) s_pos[e] = layout_pos(p, gid, (uint32_t)ep, (uint32_t)e);
+        for (int i = tid; i < N; i += kTileBlock) s_vel[i] = make_float2(0.0f, 0.0f);
+        relaid = true;
+        __syncthreads();
+    };
+    if (do_reset) relayout();
+
+    bool done = false;
+    if (p.mode == kModeStep) {
+        // apply_environment_force over the contact candidates of the previous
+        // sweep (every pair within the cutoff), then integrate_state (App. A S3-S6)
+        const uint64_t *cm = p.contact_mask + eb * N * W;
+        for (int i = tid; i < N; i += kTileBlock) {
+            const bool pre = i == tid;   // first agent of the thread: prefetched above
+            const float2 pi = s_pos[i];
+            const float2 u = pre ? u0 : action_force(p, eb * N + i);
+            float fx = 0.0f, fy = 0.0f;
+            auto visit = [&](int k, uint64_t bits) {
+                while (bits) {
+                    const int c = 64 * k + __builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    const bool ag = c < N;
+                    const float2 pj = s_pos[collider_entity(c, N)];
+                    const float dx = pi.x - pj.x, dy = pi.y - pj.y;
+                    const float d2 = dx * dx + dy * dy;
+                    const float f = contact_scale(p, d2, ag ? p.dmin_aa : p.dmin_ao);
+                    fx += f * dx;
+                    fy += f * dy;
+                }
+            };
+#pragma unroll
+            for (int k = 0; k < kPre; ++k)
+                if (k < W) visit(k, pre ? cw[k] : cm[(int64_t)i * W + k]);
+            for (int k = kPre; k < W; ++k) visit(k, cm[(int64_t)i * W + k]);
+            const float Fx = u.x + fx, Fy = u.y + fy;
+            float2 v = s_vel[i];
+            v.x = v.x * p.omd;
+            v.y = v.y * p.omd;
+            v.x = v.x + (Fx / p.mass) * p.dt;
+            v.y = v.y + (Fy / p.mass) * p.dt;
+            if (p.max_speed > 0.0f) {
+                const float sp = sqrtf(v.x * v.x + v.y * v.y);
+                if (sp > p.max_speed) {
+                    v.x = v.x / sp * p.max_speed;
+                    v.y = v.y / sp * p.max_speed;
+                }
+            }
+            s_vel[i] = v;
+            s_np[i] = make_float2(pi.x + v.x * p.dt, pi.y + v.y * p.dt);
+        }
+        __syncthreads();   // every pre-step position read
+        for (int i = tid; i < N; i += kTileBlock) s_pos[i] = s_np[i];
+        __syncthreads();
+        t += 1;
+        done = t >= p.EL;
+    }
+
+    // observation sweep of the post-step state: masks, collision counts, pairs
+#ifndef GSM_ABL_NO_SWEEP
+    int pairs = obs_sweep_any(p, s_pos, s_cost, eb, p.mode == kModeStep && !relaid);
+#else
+    int pairs = 0;
+    for (int i = tid; i < N; i += kTileBlock) s_cost[i] = 0;
+#endif
+    // reward callback: -|p_i - g_i|
+    float rpart = 0.0f;
+    for (int i = tid; i < N; i += kTileBlock) {
+        const float2 a = s_pos[i], g = s_pos[N + i];
+        const float dx = a.x - g.x, dy = a.y - g.y;
+        rpart += -sqrtf(dx * dx + dy * dy);
+    }
+    float rsum = tile_sum(rpart, s_fred);       // (its barriers also publish s_cost)
+    int csum = 0;
+    for (int i = tid; i < N; i += kTileBlock) {
+        const int cnt = s_cost[i];
+        p.cost[eb * N + i] = (float)cnt;
+        csum += cnt;
+        const float2 a = s_pos[i], g = s_pos[N + i];
+        const float dx = a.x - g.x, dy = a.y - g.y;
+        p.reward[eb * N + i] = p.shared_reward ? rsum : -sqrtf(dx * dx + dy * dy);
+    }
+    csum = tile_sum(csum, s_ired);
+    if (p.shared_reward) rsum *= (float)N;
+
+    if (p.mode == kModeStep) {
+        acc.x += rsum;
+        acc.y += (float)csum;
+        if (done && p.auto_reset) {
+            if (tid == 0) p.ep_last[b] = acc;
+            relayout();
+            pairs = obs_sweep_any(p, s_pos, s_cost, eb, false);
+        }
+    }
+    pairs = tile_sum(pairs, s_ired);
+
+    // node features [E][7] = [vx vy px py gx-px gy-py type]: agent rows every
+    // step (one thread per row), goal/obstacle rows only on layout change
+    float *nf = p.node_feat + eb * E * 7;
+    const bool full = p.mode != kModeStep || relaid;
+#ifdef GSM_ABL_NO_NF
+    if (!full) goto skip_nf;
+#endif
+    for (int i = tid; i < N; i += kTileBlock) {
+        const float2 v = s_vel[i], a = s_pos[i], g = s_pos[N + i];
+        float *row = nf + (int64_t)i * 7;
+        row[0] = v.x;
+        row[1] = v.y;
+        row[2] = a.x;
+        row[3] = a.y;
+        row[4] = g.x - a.x;
+        row[5] = g.y - a.y;
+        if (full) row[6] = 0.0f;
+    }
+    if (full) {
+        for (int e = N + tid; e < E; e += kTileBlock) {
+            const float2 a = s_pos[e];
+            float *row = nf + (int64_t)e * 7;
+            row[0] = 0.0f;
+            row[1] = 0.0f;
+            row[2] = a.x;
+            row[3] = a.y;
+            row[4] = 0.0f;
+            row[5] = 0.0f;
+            row[6] = e < 2 * N ? 1.0f : 2.0f;
+        }
+    }
+#ifdef GSM_ABL_NO_NF
+skip_nf:
+#endif
+    // state
+    if (p.mode == kModeStep || do_reset) {
+        const int ne = relaid ? E : N;
+        for (int e = tid; e < ne; e += kTileBlock) p.pos[eb * E + e] = s_pos[e];
+        for (int i = tid; i < N; i += kTileBlock) p.vel[eb * N + i] = s_vel[i];
+    }
+    const int edges = pairs + 2 * N;   // directed radius edges + agent<->goal
+    if (tid == 0) {
+        p.step_count[b] = t;
+        p.episode[b] = ep;
+        p.ep_acc[b] = acc;
+        p.done[b] = done ? 1 : 0;
+        p.edge_count[b] = edges;
+        p.block_edge_sum[b] = edges;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// edge emitter
+// ---------------------------------------------------------------------------
+// Row r's edges in entity order from its radius mask words: agent rows ->
+// agents, own goal (always), obstacles; goal rows -> own agent; obstacle rows
+// -> agents, obstacles. kWrite = false only counts.
+template <bool kWrite>
+__device__ __forceinline__ int row_edges(const DevParams &p, const float2 *s_pos, const uint64_t *rmask, int r,
+                                         int64_t off, int32_t g0) {
+    const int N = p.N, W = p.W;
+    if (r >= N && r < 2 * N) {   // goal row: goal i -> agent i
+        if (kWrite) {
+            const float2 a = s_pos[r], q = s_pos[r - N];
+            const float dx = a.x - q.x, dy = a.y - q.y;
+            p.edge_index[off] = g0 + r;
+            p.edge_index[p.edge_capacity + off] = g0 + r - N;
+            p.edge_attr[off] = sqrtf(dx * dx + dy * dy);
+        }
+        return 1;
+    }
+    const int m = r < N ? r : r - N;             // collider row
+    const uint64_t *row = rmask + (int64_t)m * W;
+    if (!kWrite) {
+        int n = r < N ? 1 : 0;
+        for (int k = 0; k < W; ++k) n += __popcll(row[k]);
+        return n;
+    }
+    const float2 a = s_pos[r];
+    int n = 0;
+    auto put = [&](int dst) {
+        const float2 q = s_pos[dst];
+        const float dx = a.x - q.x, dy = a.y - q.y;
+        p.edge_index[off + n] = g0 + r;
+        p.edge_index[p.edge_capacity + off + n] = g0 + dst;
+        p.edge_attr[off + n] = sqrtf(dx * dx + dy * dy);
+        ++n;
+    };
+    bool goal_done = r >= N;
+    for (int k = 0; k < W; ++k) {
+        uint64_t bits = row[k];
+        while (bits) {
+            const int c = 64 * k + __builtin_ctzll(bits);
+            bits &= bits - 1;
+            if (!goal_done && c >= N) {   // own goal sits between agents and obstacles
+                put(N + r);
+                goal_done = true;
+            }
+            put(collider_entity(c, N));
+        }
+    }
+    if (!goal_done) put(N + r);
+    return n;
+}
+
+__global__ __launch_bounds__(kTileBlock) void gsm_emit_tile_kernel(DevParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int E = p.E;
+    float2 *s_pos = (float2 *)smem;
+    int *s_red = (int *)(s_pos + E);          // [kTileWaves]
+    const int64_t eb = b;
+    const uint64_t *rmask = p.row_mask + eb * p.M * p.W;
+    // global offset: edges of envs [0, b)  (host keeps totals < 2^31)
+    int before = 0;
+    for (int k = tid; k < b; k += kTileBlock) before += p.edge_count[k];
+    for (int e = tid; e < E; e += kTileBlock) s_pos[e] = p.pos[eb * E + e];
+    const int64_t off = tile_sum(before, s_red);
+    // this thread's rows: a contiguous run (row-major order across the workgroup)
+    const int R = (E + kTileBlock - 1) / kTileBlock;
+    const int r0 = tid * R, r1 = min(E, r0 + R);
+    const int32_t g0 = (int32_t)(eb * E);
+    int mine = 0;
+    for (int r = r0; r < r1; ++r) mine += row_edges<false>(p, s_pos, rmask, r, 0, g0);
+    // workgroup exclusive scan of the per-thread counts
+    const int incl = wave_scan(mine);
+    __syncthreads();
+    if (lane == 63) s_red[wave] = incl;
+    __syncthreads();
+    int base = incl - mine;
+    for (int w = 0; w < wave; ++w) base += s_red[w];
+    int64_t o = off + base;
+    for (int r = r0; r < r1; ++r) o += row_edges<true>(p, s_pos, rmask, r, o, g0);
+    if (tid == 0) {
+        p.edge_ptr[b] = off;
+        if (b == p.B - 1) p.edge_ptr[p.B] = off + p.edge_count[b];
+    }
+}
+
+const void *step_tile_kernel_fn() { return reinterpret_cast<const void *>(&gsm_step_tile_kernel); }
+const void *emit_tile_kernel_fn() { return reinterpret_cast<const void *>(&gsm_emit_tile_kernel); }
+
+}  // namespace gsm

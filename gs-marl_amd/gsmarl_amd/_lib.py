@@ -39,6 +39,7 @@ class GsmSizes(C.Structure):
         ("n_entities", C.c_int32), ("node_feat_dim", C.c_int32), ("obs_dim", C.c_int32),
         ("envs_per_block", C.c_int32), ("n_blocks", C.c_int32), ("max_edges_per_env", C.c_int32),
         ("edge_capacity", C.c_int64), ("n_colliders", C.c_int32), ("n_targets", C.c_int32),
+        ("mask_words", C.c_int32),
     ]
 
 

@@ -67,8 +67,9 @@ class GpuBatchEnv:
             edge_index=torch.zeros(2, cap, dtype=i32, device=dev),
             edge_attr=torch.zeros(cap, dtype=f32, device=dev),
             # derived state (refreshed by every reset/step/observe)
-            row_mask=torch.zeros(B, self.sizes.n_colliders, dtype=torch.int64, device=dev),
-            contact_mask=torch.zeros(B, N, dtype=torch.int64, device=dev),
+            row_mask=torch.zeros(B, self.sizes.n_colliders * self.sizes.mask_words, dtype=torch.int64,
+                                 device=dev),
+            contact_mask=torch.zeros(B, N * self.sizes.mask_words, dtype=torch.int64, device=dev),
             # ragged batches: N_env | scenario << 8, and the LSA slot of each agent
             env_shape=torch.zeros(B, dtype=i32, device=dev),
             assign=torch.full((B, N), -1, dtype=i32, device=dev),

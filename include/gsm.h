@@ -101,8 +101,9 @@ typedef struct gsm_sizes {
     int32_t n_blocks;         /* length of block_edge_sum                    */
     int32_t max_edges_per_env;
     int64_t edge_capacity;    /* length of edge_attr and of each edge_index row */
-    int32_t n_colliders;      /* M = row_mask entries per env (agents + obstacles) */
+    int32_t n_colliders;      /* M: collider rows per env (agents + obstacles)  */
     int32_t n_targets;        /* T_max: goal/landmark rows per env            */
+    int32_t mask_words;       /* W: uint64 words per mask row, ceil(M / 64)   */
 } gsm_sizes;
 
 /* Caller-owned device buffers (all contiguous, row-major). */
@@ -126,8 +127,8 @@ typedef struct gsm_buffers {
     float *edge_attr;         /* [edge_capacity]    distance                  */
     /* derived state, valid for the positions in `pos` after any reset/step/
      * observe; a caller that rewrites `pos`/`vel` must call gsm_observe      */
-    uint64_t *row_mask;       /* [B][M] radius adjacency rows (bit = collider) */
-    uint64_t *contact_mask;   /* [B][N] contact candidates of each agent        */
+    uint64_t *row_mask;       /* [B][M][W] radius adjacency rows (bit = collider) */
+    uint64_t *contact_mask;   /* [B][N][W] contact candidates of each agent        */
     /* ragged scenarios only (may be NULL for navigation) */
     int32_t *env_shape;       /* [B]    N_env | scenario << 8 (set at every layout) */
     int32_t *assign;          /* [B][N] polygon/line slot of each agent (LSA), -1 else */

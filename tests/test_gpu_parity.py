@@ -109,7 +109,8 @@ def _inject_random(env, ocfg, L, seed, vel_scale=1.0):
 
 
 @pytest.mark.parametrize("N,No,B,L", [(3, 3, 64, 0.35), (24, 24, 256, 1.2), (24, 24, 256, 2.83), (5, 2, 37, 0.5), (32, 32, 9, 1.6), (24, 24, 8, 0.3), (8, 8, 16, 0.2),
-                                      (96, 96, 16, 3.0), (64, 0, 8, 1.0), (65, 7, 8, 1.5), (1, 0, 4, 1.0)])
+                                      (96, 96, 16, 3.0), (64, 0, 8, 1.0), (65, 7, 8, 1.5), (1, 0, 4, 1.0),
+                                      (600, 10, 2, 8.0), (40, 40, 8, 0.9)])
 def test_one_step_physics_parity(N, No, B, L):
     env, ocfg = _env(n_agents=N, n_obstacles=No, n_envs=B, episode_length=1000)
     env.reset(seed=0)
@@ -185,7 +186,7 @@ def test_boundary_predicates_exact():
 
 
 # ------------------------------------------------------------- episodes
-@pytest.mark.parametrize("N,B", [(3, 1), (3, 256), (24, 64)])
+@pytest.mark.parametrize("N,B", [(3, 1), (3, 256), (24, 64), (96, 16), (40, 8)])
 def test_episode_rollout_stepwise(N, B):
     """A 2.5-episode rollout with auto-reset; each step is checked against the
     fp64 oracle started from the kernel's own pre-step state."""
@@ -284,6 +285,30 @@ def test_kernel_only_graphs():
     assert torch.equal(eager["edge_index"][:, :n], env.t["edge_index"][:, :n])
     assert torch.equal(eager["edge_attr"][:n], env.t["edge_attr"][:n])
     assert env.graph_kernel_ms(3)[1] > 0
+
+
+def test_c3_size_sample():
+    """BASELINE C3 (96 agents x 1024 envs, tile path): three steps, then the
+    oracle on a sample of envs from the kernel's own state."""
+    env, ocfg = _env(n_agents=96, n_envs=1024, episode_length=1000)
+    env.reset(seed=2)
+    rng = np.random.default_rng(2)
+    for _ in range(3):
+        st = {k: _np(v) for k, v in env.get_state().items()}
+        a = rng.integers(0, 5, size=(1024, 96))
+        out = env.step(torch.from_numpy(a.astype(np.int32)).to(DEV))
+        torch.cuda.synchronize()
+    idx = np.array([0, 1, 511, 1022, 1023])
+    p64, v64 = br.physics(ocfg, st["pos"][idx].astype(np.float64), st["vel"][idx].astype(np.float64),
+                          a[idx], 1, np.float64)
+    assert_state_close(_np(env.t["pos"])[idx], p64, "pos")
+    assert_state_close(_np(env.t["vel"])[idx], v64, "vel")
+    pos = _np(env.t["pos"])
+    ptr, ei, attr = br.edges(ocfg, pos, np.float32)
+    assert np.array_equal(_np(out["edge_ptr"]), ptr)
+    assert np.array_equal(_np(out["edge_index"]), ei)
+    _, c = br.reward_cost(ocfg, pos, np.float32)
+    assert np.array_equal(_np(out["cost"]), c)
 
 
 def test_headline_size_properties():

@@ -7,9 +7,9 @@ if [ "$mode" = build ]; then
   mkdir -p gs-marl_amd/gsmarl_amd/lib/ablate
   for spec in "$@"; do
     name=${spec%%:*}; flags=${spec#*:}
+    srcs=$(python -c "import __graft_entry__ as g; print(' '.join(str(g.CSRC / s) for s in g.SOURCES))")
     /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared $flags \
-      -Iinclude -Igs-marl_amd/csrc gs-marl_amd/csrc/gsm_kernels.hip gs-marl_amd/csrc/gsm_seg_kernels.hip \
-      gs-marl_amd/csrc/gsm_abi.hip -o gs-marl_amd/gsmarl_amd/lib/ablate/$name.so || exit 1
+      -Iinclude -Igs-marl_amd/csrc $srcs -o gs-marl_amd/gsmarl_amd/lib/ablate/$name.so || exit 1
     echo built $name
   done
 else
