@@ -303,7 +303,7 @@ def main():
         other = kern["emit" if dom == "step" else "step"]
         roofline = dict(kernel=k["kernel"], bound="hbm", achieved=round(k["gbs"], 1), peak=HBM_PEAK_GBS,
                         unit="GB/s", frac=round(k["gbs"] / HBM_PEAK_GBS, 4),
-                        traffic=pmc_traffic(f"{dom}:N{N}:B{B}"),
+                        traffic=pmc_traffic(f"{dom}:{cfg.scenario}:N{N}:B{B}"),
                         algorithmic_bytes_per_launch=int(k["bytes"]), mean_launch_us=round(k["ms"] * 1e3, 3),
                         timing=f"HIP events around {L} back-to-back graph launches of the kernel",
                         other_kernel=dict(kernel=other["kernel"], achieved=round(other["gbs"], 1),
