@@ -12,7 +12,8 @@ Same names, same ``reset()`` / ``step(action_n)`` methods. Return conventions
 graph variant follows InforMARL ``(obs_n, agent_id_n, node_obs_n, adj_n, ...)``.
 
 With ``n_envs == 1`` the values are per-agent lists of numpy arrays exactly as
-a single MPE env returns them. With ``n_envs > 1`` they are stacked numpy
+a single MPE env returns them (ragged scenarios: the env's own N_env agents;
+actions for N_env agents are padded with no-ops). With ``n_envs > 1`` they are stacked numpy
 arrays in the MAPPO vec-env shapes (obs [B,N,6], reward [B,N,1], done [B,N]).
 Either way ``self.last`` keeps the device tensors of the latest call, and
 ``graph()`` returns the batched COO graph without building dense adjacency.
@@ -49,6 +50,11 @@ class MultiAgentEnv:
         self.adj_observation_space = [Box(0, np.inf, (E, E)) for _ in range(self.n)]
         self.agent_id_observation_space = [Box(0, self.n, (1,)) for _ in range(self.n)]
         self.last = None
+        self.n_active = self.n   # ragged single env: its N_env after reset
+
+    def _refresh_active(self, out):
+        if self.cfg.ragged and self.num_envs == 1:
+            self.n_active = int(out["n_agents_env"][0].item())
 
     # ---------------------------------------------------------------- actions
     def _to_actions(self, action_n) -> torch.Tensor:
@@ -69,13 +75,16 @@ class MultiAgentEnv:
                 a = a.unsqueeze(0)
             if a.dim() == 3 and a.shape[-1] == 1:
                 a = a[..., 0]
+        if B == 1 and a.dim() >= 2 and a.shape[0] == 1 and a.shape[1] < N:   # ragged env: pad with no-ops
+            pad = torch.zeros((1, N - a.shape[1], *a.shape[2:]), dtype=a.dtype, device=dev)
+            a = torch.cat([a, pad], dim=1)
         return a.reshape(B, N, *a.shape[2:]).contiguous()
 
     # --------------------------------------------------------------- outputs
     def _per_agent(self, x: np.ndarray):
         """[B, N, ...] -> per-agent list (n_envs == 1) or the stacked array."""
         if self.num_envs == 1:
-            return [x[0, i] for i in range(self.n)]
+            return [x[0, i] for i in range(self.n_active)]
         return x
 
     def _obs(self, out):
@@ -84,24 +93,24 @@ class MultiAgentEnv:
     def _reward(self, out):
         r = out["reward"].cpu().numpy()
         if self.num_envs == 1:
-            return [float(v) for v in r[0]]
+            return [float(v) for v in r[0, : self.n_active]]
         return r[..., None]
 
     def _cost(self, out):
         c = out["cost"].cpu().numpy()
         if self.num_envs == 1:
-            return [float(v) for v in c[0]]
+            return [float(v) for v in c[0, : self.n_active]]
         return c[..., None]
 
     def _done(self, out):
         d = out["done"].cpu().numpy().astype(bool)
         if self.num_envs == 1:
-            return [bool(d[0])] * self.n
+            return [bool(d[0])] * self.n_active
         return np.repeat(d[:, None], self.n, axis=1)
 
     def _info(self, out, cost=None):
         if self.num_envs == 1:
-            infos = [{} for _ in range(self.n)]
+            infos = [{} for _ in range(self.n_active)]
             if cost is not None:
                 for i, c in enumerate(cost):
                     infos[i]["cost"] = c
@@ -118,6 +127,7 @@ class MultiAgentEnv:
         out = self.batch.reset(seed=seed, sync_edges=self.with_graph)
         self.current_step = 0
         self.last = out
+        self._refresh_active(out)
         return self._obs(out)
 
     def step(self, action_n):
@@ -163,7 +173,8 @@ class MultiAgentGraphConstrainEnv(MultiAgentConstrainEnv):
         adj = self._dense_adj(out)
         aid = out["agent_id"].cpu().numpy()[..., None]
         if self.num_envs == 1:
-            return ([aid[0, i] for i in range(self.n)], [node[0]] * self.n, [adj[0]] * self.n)
+            n = self.n_active
+            return ([aid[0, i] for i in range(n)], [node[0]] * n, [adj[0]] * n)
         B, N = self.num_envs, self.n
         return (aid, np.repeat(node[:, None], N, axis=1), np.repeat(adj[:, None], N, axis=1))
 

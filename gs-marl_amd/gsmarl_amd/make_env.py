@@ -12,9 +12,21 @@ ENV_CLASSES = {
 }
 
 
+# the reference's scenario module names (SOURCES.txt:21-25) -> scenario
+SCENARIO_ALIASES = {
+    "exp1": "navigation", "exp2": "navigation", "navigation": "navigation",
+    "simple_formation": "polygon", "formation": "polygon", "polygon": "polygon",
+    "simple_line": "line", "line": "line", "mixed": "mixed",
+}
+
+
 def make_env(scenario_name: str = "navigation", env_class: str = "MultiAgentGraphConstrainEnv",
              device="cuda", **params):
-    cfg = EnvConfig(scenario=scenario_name, **params)
+    try:
+        scenario = SCENARIO_ALIASES[scenario_name]
+    except KeyError:
+        raise ValueError(f"unknown scenario {scenario_name!r}; have {sorted(SCENARIO_ALIASES)}") from None
+    cfg = EnvConfig(scenario=scenario, **params)
     try:
         cls = ENV_CLASSES[env_class]
     except KeyError:

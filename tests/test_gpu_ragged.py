@@ -211,3 +211,23 @@ def test_config_validation():
         GpuBatchEnv(EnvConfig(scenario="polygon", n_agents=33, n_envs=2), DEV)
     with pytest.raises(GsmError):
         GpuBatchEnv(EnvConfig(scenario="mixed", n_agents=8, n_obstacles=3, n_envs=2), DEV)
+
+
+def test_dropin_ragged_single_env():
+    """Drop-in classes on ragged scenarios: per-agent lists of the env's own
+    N_env agents; actions for N_env agents are padded with no-ops."""
+    from gsmarl_amd import make_env
+    env = make_env("simple_formation", "MultiAgentGraphConstrainEnv", device=DEV, n_agents=5, n_envs=1)
+    obs, aid, node, adj = env.reset(seed=3)
+    assert len(obs) == 5 and node[0].shape == (6, 7) and adj[0].shape == (6, 6)
+    obs, aid, node, adj, rew, cost, done, info = env.step([np.eye(5)[1]] * 5)
+    assert len(rew) == 5 and len(cost) == 5 and all(r <= 0 for r in rew)
+    mixed = make_env("mixed", "MultiAgentConstrainEnv", device=DEV, n_agents=24, n_envs=1, env_base=4, seed=9)
+    o = mixed.reset(seed=9)
+    n, scn = rr.env_shapes(rr.make_cfg(scenario="mixed", n_agents=24, n_envs=1, env_base=4, seed=9), 9)
+    assert len(o) == int(n[0]) == mixed.n_active
+    o, r, c, d, inf = mixed.step(list(range(5)) * (int(n[0]) // 5) + [0] * (int(n[0]) % 5))
+    assert len(r) == int(n[0]) and len(inf) == int(n[0])
+    line = make_env("simple_line", "MultiAgentEnv", device=DEV, n_agents=4, n_envs=3)
+    o = line.reset(seed=1)
+    assert o.shape == (3, 4, 6)
