@@ -46,32 +46,38 @@ __device__ __forceinline__ double rl_d(double v, int l) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-// One step of the (cost, key) argmin over lanes [0, 32): take the DPP
-// neighbour's pair when its cost is smaller, or equal with a larger key.
-// Lanes a control does not write keep their own pair (old = src).
+// DPP reductions over lanes [0, 32) (the assignment never uses more): within
+// rows of 16 via quad perms and half-row / row mirrors, then row 0 broadcast
+// into row 1 (row_bcast:15); lane 31 holds the result. Lanes a control does
+// not write keep their own value (old = src).
 template <int kCtrl, int kRowMask = 0xf>
-__device__ __forceinline__ void argmin_step(double &c, int &k) {
-    const long long bits = __double_as_longlong(c);
+__device__ __forceinline__ double dpp_d(double v) {
+    const long long bits = __double_as_longlong(v);
     const int lo = (int)(uint32_t)bits, hi = (int)(uint32_t)(bits >> 32);
     const int lo2 = __builtin_amdgcn_update_dpp(lo, lo, kCtrl, kRowMask, 0xf, false);
     const int hi2 = __builtin_amdgcn_update_dpp(hi, hi, kCtrl, kRowMask, 0xf, false);
-    const int k2 = __builtin_amdgcn_update_dpp(k, k, kCtrl, kRowMask, 0xf, false);
-    const double c2 = __longlong_as_double((long long)(((uint64_t)(uint32_t)hi2 << 32) | (uint32_t)lo2));
-    const bool take = c2 < c || (c2 == c && k2 > k);
-    c = take ? c2 : c;
-    k = take ? k2 : k;
+    return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi2 << 32) | (uint32_t)lo2));
 }
-// (cost, key) pair minimal in cost, then maximal in key, over lanes [0, 32):
-// DPP within rows of 16 (quad perms, half-row and row mirrors), then row 0's
-// result broadcast into row 1 (row_bcast:15); lane 31 holds the answer.
-__device__ __forceinline__ void argmin32(double &c, int &k) {
-    argmin_step<0xB1>(c, k);          // quad_perm [1,0,3,2]
-    argmin_step<0x4E>(c, k);          // quad_perm [2,3,0,1]
-    argmin_step<0x141>(c, k);         // row_half_mirror
-    argmin_step<0x140>(c, k);         // row_mirror
-    argmin_step<0x142, 0xa>(c, k);    // row_bcast:15 -> rows 1, 3
-    c = rl_d(c, 31);
-    k = __builtin_amdgcn_readlane(k, 31);
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ int dpp_keep(int v) {
+    return __builtin_amdgcn_update_dpp(v, v, kCtrl, kRowMask, 0xf, false);
+}
+// exact minimum (values are never NaN; -0 and +0 compare equal downstream)
+__device__ __forceinline__ double min32(double v) {
+    v = fmin(v, dpp_d<0xB1>(v));          // quad_perm [1,0,3,2]
+    v = fmin(v, dpp_d<0x4E>(v));          // quad_perm [2,3,0,1]
+    v = fmin(v, dpp_d<0x141>(v));         // row_half_mirror
+    v = fmin(v, dpp_d<0x140>(v));         // row_mirror
+    v = fmin(v, dpp_d<0x142, 0xa>(v));    // row_bcast:15 -> rows 1, 3
+    return rl_d(v, 31);
+}
+__device__ __forceinline__ int max32(int v) {
+    v = max(v, dpp_keep<0xB1>(v));
+    v = max(v, dpp_keep<0x4E>(v));
+    v = max(v, dpp_keep<0x141>(v));
+    v = max(v, dpp_keep<0x140>(v));
+    v = max(v, dpp_keep<0x142, 0xa>(v));
+    return __builtin_amdgcn_readlane(v, 31);
 }
 __device__ __forceinline__ int first_lane(uint64_t m) { return __builtin_ctzll(m); }
 
@@ -172,16 +178,19 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
             }
             // scipy scans `remaining` in order and keeps the first minimum
             // unless a later equal one is unassigned: the last unassigned
-            // minimum in scan order if any, else the first minimum. As a
-            // total order: cost, then key = 64 + pos (unassigned) or
-            // 63 - pos (assigned), larger key winning; keys are distinct.
-            const int key = rem ? (row4col == -1 ? 64 + rpos : 63 - rpos) : -1;
-            double m = rem ? spc : kInf;
-            int kb = key;
-            argmin32(m, kb);
-            const uint64_t win = __ballot(rem && key == kb);
-            if (!win) break;
-            const int jsel = first_lane(win);
+            // minimum in scan order if any, else the first minimum. With
+            // continuous costs the minimum is almost always unique; ties take
+            // one more reduction over key = 64 + pos (unassigned) or 63 - pos
+            // (assigned), larger key winning (keys are distinct).
+            const double m = min32(rem ? spc : kInf);
+            const uint64_t cand = __builtin_amdgcn_ballot_w64(rem && spc == m);
+            if (!cand) break;
+            int jsel = first_lane(cand);
+            if (cand & (cand - 1)) {
+                const int key = (rem && spc == m) ? (row4col == -1 ? 64 + rpos : 63 - rpos) : -1;
+                const int kb = max32(key);
+                jsel = first_lane(__builtin_amdgcn_ballot_w64(key == kb));
+            }
             minVal = m;
             const int r4c = __builtin_amdgcn_readlane(row4col, jsel);
             const int at = __builtin_amdgcn_readlane(rpos, jsel);

@@ -232,9 +232,77 @@ __device__ __forceinline__ void store_row(float *nf, float2 v, float2 pos, float
     nf[6] = type;
 }
 
+// Writes the env's edges from the lanes' radius row masks, given the env's
+// global offset: row offsets in entity order (agent rows, goal rows,
+// obstacle rows) by a segment scan of the row counts, then each lane writes
+// its row (agent columns, own goal, obstacle columns); agent lanes also
+// write the goal rows.
+template <int kN, int kNo, int kG>
+__device__ __forceinline__ void emit_rows(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L,
+                                          const float2 *s_pos, uint64_t mask, int64_t env_off) {
+    const int N = s.N, E = s.E;
+    const int m = L.m;
+    const int64_t eb = L.live ? L.b : 0;
+    // row offsets in entity order: agent rows, goal rows, obstacle rows
+    const int c = __popcll(mask) + (L.agent ? 1 : 0);
+    int incl, a_total;
+    if constexpr (kG == 1) {
+        incl = wave_scan(c);
+        a_total = __builtin_amdgcn_readlane(incl, N - 1);
+    } else {
+        incl = seg_scan(c, m);
+        a_total = __shfl(incl, L.base + N - 1);
+    }
+    int64_t o = env_off + incl - c + (m >= N ? N : 0);
+    if (!L.live) return;
+
+    const float2 pm = s_pos[row_entity(m, N)];
+    int32_t *src = p.edge_index, *dst = p.edge_index + p.edge_capacity;
+    float *attr = p.edge_attr;
+    const int32_t g0 = (int32_t)(eb * E);
+    const int32_t gs = g0 + row_entity(m, N);
+    const uint64_t agent_bits = N >= 64 ? ~0ull : ((1ull << N) - 1);
+    uint64_t lo = mask & agent_bits, hi = mask & ~agent_bits;
+    while (lo) {
+        const int j = __builtin_ctzll(lo);
+        lo &= lo - 1;
+        const float2 q = s_pos[j];
+        const float dx = pm.x - q.x, dy = pm.y - q.y;
+        src[o] = gs;
+        dst[o] = g0 + j;
+        attr[o] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+        ++o;
+    }
+    if (L.agent) {
+        const float2 g = s_pos[N + m];
+        const float dx = pm.x - g.x, dy = pm.y - g.y;
+        const float d = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+        src[o] = gs;                    // agent m -> its goal
+        dst[o] = g0 + N + m;
+        attr[o] = d;
+        ++o;
+        const int64_t og = env_off + a_total + m;
+        src[og] = g0 + N + m;           // goal row: goal m -> agent m
+        dst[og] = gs;
+        attr[og] = d;
+    }
+    while (hi) {
+        const int j = __builtin_ctzll(hi);
+        hi &= hi - 1;
+        const float2 q = s_pos[N + j];
+        const float dx = pm.x - q.x, dy = pm.y - q.y;
+        src[o] = gs;
+        dst[o] = g0 + N + j;
+        attr[o] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+        ++o;
+    }
+}
+
 // ---------------------------------------------------------------------------
 #ifdef GSM_STEP_SGPR   // experiment: SGPR budget (residency = floor(800 / (ceil(sgpr/16)*16 + 16)) waves/SIMD)
 #define GSM_STEP_ATTR __attribute__((amdgpu_num_sgpr(GSM_STEP_SGPR)))
+#elif defined(GSM_STEP_OCC)   // experiment: ask for GSM_STEP_OCC waves per SIMD
+#define GSM_STEP_ATTR __attribute__((amdgpu_waves_per_eu(GSM_STEP_OCC)))
 #else
 #define GSM_STEP_ATTR
 #endif
@@ -463,6 +531,9 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
         }
     }
 
+#ifdef GSM_ABL_FUSED_PADDED   // timing-only: emit here at a fixed per-env stride
+    emit_rows<kN, kNo, kG>(p, s, L, s_pos, row, (int64_t)(L.live ? L.b : 0) * (p.edge_capacity / p.B));
+#endif
     GSM_STAMP(p, wid, 5);
     // edge count (radius rows + goal edges both ways)
     const int edges = __popcll(row) + ((L.live && m == 0) ? 2 * N : 0);
@@ -579,64 +650,7 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
     }
     GSM_STAMP(p, wid, 2);
 
-    // row offsets in entity order: agent rows, goal rows, obstacle rows
-    const int c = __popcll(mask) + (L.agent ? 1 : 0);
-    int incl, a_total;
-    if constexpr (kG == 1) {
-        incl = wave_scan(c);
-        a_total = __builtin_amdgcn_readlane(incl, N - 1);
-    } else {
-        incl = seg_scan(c, m);
-        a_total = __shfl(incl, L.base + N - 1);
-    }
-    int64_t o = env_off + incl - c + (m >= N ? N : 0);
-    GSM_STAMP(p, wid, 3);
-    if (!L.live) return;
-#ifdef GSM_ABL_NO_EMIT_STORES   // timing-only: every edge store hits one slot
-    o = 0;
-    env_off = 0;
-#endif
-
-    const float2 pm = s_pos[row_entity(m, N)];
-    int32_t *src = p.edge_index, *dst = p.edge_index + p.edge_capacity;
-    float *attr = p.edge_attr;
-    const int32_t g0 = (int32_t)(eb * E);
-    const int32_t gs = g0 + row_entity(m, N);
-    const uint64_t agent_bits = N >= 64 ? ~0ull : ((1ull << N) - 1);
-    uint64_t lo = mask & agent_bits, hi = mask & ~agent_bits;
-    while (lo) {
-        const int j = __builtin_ctzll(lo);
-        lo &= lo - 1;
-        const float2 q = s_pos[j];
-        const float dx = pm.x - q.x, dy = pm.y - q.y;
-        src[o] = gs;
-        dst[o] = g0 + j;
-        attr[o] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-        ++o;
-    }
-    if (L.agent) {
-        const float2 g = s_pos[N + m];
-        const float dx = pm.x - g.x, dy = pm.y - g.y;
-        const float d = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-        src[o] = gs;                    // agent m -> its goal
-        dst[o] = g0 + N + m;
-        attr[o] = d;
-        ++o;
-        const int64_t og = env_off + a_total + m;
-        src[og] = g0 + N + m;           // goal row: goal m -> agent m
-        dst[og] = gs;
-        attr[og] = d;
-    }
-    while (hi) {
-        const int j = __builtin_ctzll(hi);
-        hi &= hi - 1;
-        const float2 q = s_pos[N + j];
-        const float dx = pm.x - q.x, dy = pm.y - q.y;
-        src[o] = gs;
-        dst[o] = g0 + N + j;
-        attr[o] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-        ++o;
-    }
+    emit_rows<kN, kNo, kG>(p, s, L, s_pos, mask, env_off);
     GSM_STAMP(p, wid, 4);
     GSM_RSTAMP(p, wid, 9);
 }
