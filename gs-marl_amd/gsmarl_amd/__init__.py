@@ -4,8 +4,10 @@ from .config import EnvConfig
 from .batch import GpuBatchEnv
 from .environment import MultiAgentConstrainEnv, MultiAgentEnv, MultiAgentGraphConstrainEnv
 from .make_env import make_env
+from .vec_env import GpuGraphVecEnv, make_eval_env, make_train_env
 from . import distributed
 
 __version__ = "0.1.0"
 __all__ = ["EnvConfig", "GpuBatchEnv", "MultiAgentEnv", "MultiAgentConstrainEnv",
-           "MultiAgentGraphConstrainEnv", "make_env", "distributed"]
+           "MultiAgentGraphConstrainEnv", "make_env", "GpuGraphVecEnv", "make_train_env", "make_eval_env",
+           "distributed"]
