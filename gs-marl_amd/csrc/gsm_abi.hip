@@ -212,8 +212,33 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
 
 hipStream_t as_stream(void *s) { return reinterpret_cast<hipStream_t>(s); }
 
+// Point a launch's outputs at `o` (NULL members keep the bound buffers).
+int redirect(gsm_handle *h, gsm::DevParams *p, const gsm_outputs *o) {
+    if (!o) return GSM_OK;
+    if (o->edge_index && o->edge_capacity < 1)
+        return fail(h, GSM_EINVAL, "redirected edge_index needs edge_capacity >= 1");
+    if (o->edge_index && o->edge_capacity >= (int64_t)1 << 31)
+        return fail(h, GSM_EINVAL, "edge_capacity must be < 2^31");
+    if (!!o->edge_index != !!o->edge_attr)
+        return fail(h, GSM_EINVAL, "edge_index and edge_attr are redirected together");
+    if (o->node_feat) p->node_feat = o->node_feat;
+    if (o->reward) p->reward = o->reward;
+    if (o->cost) p->cost = o->cost;
+    if (o->done) p->done = o->done;
+    if (o->edge_count) p->edge_count = o->edge_count;
+    if (o->edge_ptr) p->edge_ptr = o->edge_ptr;
+    if (o->edge_index) {
+        p->edge_index = o->edge_index;
+        p->edge_attr = o->edge_attr;
+        p->edge_capacity = o->edge_capacity;
+    }
+    if (o->assign) p->assign = o->assign;
+    p->nf_full = 1;
+    return GSM_OK;
+}
+
 int launch(gsm_handle *h, int mode, const void *actions, int fmt, const uint8_t *mask, int reseed,
-           hipStream_t s) {
+           hipStream_t s, const gsm_outputs *out = nullptr) {
     if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
     if (!h->bound) return fail(h, GSM_ESTATE, "gsm_bind has not been called");
     if (mode == GSM_MODE_STEP) {
@@ -221,6 +246,8 @@ int launch(gsm_handle *h, int mode, const void *actions, int fmt, const uint8_t 
         if (fmt < GSM_ACT_ONEHOT || fmt > GSM_ACT_CONT) return fail(h, GSM_EINVAL, "bad action_fmt");
     }
     gsm::DevParams p = h->dp;
+    const int rc = redirect(h, &p, out);
+    if (rc) return rc;
     p.mode = mode;
     p.actions = actions;
     p.action_fmt = fmt;
@@ -345,8 +372,32 @@ int gsm_observe(gsm_handle *h, void *stream) {
     return launch(h, GSM_MODE_OBSERVE, nullptr, 0, nullptr, 0, as_stream(stream));
 }
 
+int gsm_step_into(gsm_handle *h, const void *actions, int action_fmt, const gsm_outputs *out, void *stream) {
+    if (!out) return fail(h, GSM_EINVAL, "outputs is NULL");
+    return launch(h, GSM_MODE_STEP, actions, action_fmt, nullptr, 0, as_stream(stream), out);
+}
+
+int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream) {
+    if (!out) return fail(h, GSM_EINVAL, "outputs is NULL");
+    return launch(h, GSM_MODE_OBSERVE, nullptr, 0, nullptr, 0, as_stream(stream), out);
+}
+
+static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_t stride, int32_t n_actions,
+                        int32_t n_steps, int action_fmt, int flags, const gsm_outputs *per_step);
+
 int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t stride,
                       int32_t n_actions, int32_t n_steps, int action_fmt, int flags) {
+    return capture_impl(h, slot, actions, stride, n_actions, n_steps, action_fmt, flags, nullptr);
+}
+
+int gsm_graph_capture_into(gsm_handle *h, int32_t slot, const void *actions, int64_t stride,
+                           int32_t n_actions, int32_t n_steps, int action_fmt, const gsm_outputs *per_step) {
+    if (!per_step) return fail(h, GSM_EINVAL, "per_step outputs is NULL");
+    return capture_impl(h, slot, actions, stride, n_actions, n_steps, action_fmt, 0, per_step);
+}
+
+static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_t stride, int32_t n_actions,
+                        int32_t n_steps, int action_fmt, int flags, const gsm_outputs *per_step) {
     if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
     if (!h->bound) return fail(h, GSM_ESTATE, "gsm_bind has not been called");
     if (bad_slot(slot)) return fail(h, GSM_EINVAL, "bad graph slot");
@@ -410,8 +461,17 @@ int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t 
     };
     what = "event node";
     e = n_ev ? add_event(sl.events[0]) : hipSuccess;
+    const gsm::DevParams p_bound = p;
     for (int t = 0; t < n_steps && e == hipSuccess; ++t) {
         at = t;
+        if (per_step) {
+            p = p_bound;
+            const int rc = redirect(h, &p, &per_step[t]);
+            if (rc) {
+                drop_slot(sl);
+                return rc;
+            }
+        }
         if (kern & GSM_GRAPH_STEP) {
             p.actions = (const char *)actions + (int64_t)(t % n_actions) * stride;
             what = "step kernel node";

@@ -29,6 +29,7 @@ struct DevParams {
     int32_t T;             // ragged: target rows per env (T_max); N, No, E, M are the padded maxima
     int32_t n_min;         // ragged mixed: smallest N_env
     int32_t W;             // uint64 words per mask row (tile path: ceil(M/64))
+    int32_t nf_full;       // write every node-feature row (redirected outputs)
     int32_t G;             // envs per wave (segmented path), 1 otherwise
     uint32_t seed_lo, seed_hi;
     int64_t env_base;

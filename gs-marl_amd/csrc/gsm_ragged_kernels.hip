@@ -365,7 +365,8 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
     }
 
     // node features [v, p, target - p, type]; target = own goal / assigned slot
-    const bool full = p.mode != kModeStep || relaid;
+    const bool full = p.mode != kModeStep || relaid;   // positions / velocities of every row
+    const bool full_nf = full || p.nf_full;              // static node-feature rows
     float2 tgt = tp;
     if (s.scn != kScnNav) {
         const int src = sigma < 0 ? 0 : sigma;
@@ -379,11 +380,11 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
         nf[3] = cp.y;
         nf[4] = tgt.x - cp.x;
         nf[5] = tgt.y - cp.y;
-        if (full) nf[6] = 0.0f;
+        if (full_nf) nf[6] = 0.0f;
     }
     if (lane < Nmax) p.assign[eb * Nmax + lane] = (lane < s.N && s.scn != kScnNav) ? sigma : -1;
 
-    if (full) {
+    if (full_nf) {
         // every storage row: positions (padding 0) and the static node rows
         for (int q = lane; q < Emax; q += kWave) s_pos[q] = make_float2(0.0f, 0.0f);
         wave_sync();
@@ -392,7 +393,7 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
         wave_sync();
         for (int q = lane; q < Emax; q += kWave) {
             const float2 pq = s_pos[q];
-            pos_b[q] = pq;
+            if (full) pos_b[q] = pq;
             if (q < s.N) continue;   // live agent rows written above
             float type;
             if (q < Nmax) type = -1.0f;
@@ -407,6 +408,8 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
             nf[5] = 0.0f;
             nf[6] = type;
         }
+    }
+    if (full) {
         if (lane < Nmax) p.vel[eb * Nmax + lane] = lane < s.N ? v : make_float2(0.0f, 0.0f);
     } else if (lane < s.N) {
         pos_b[lane] = cp;
@@ -464,11 +467,13 @@ __device__ void ragged_env_emit(const DevParams &p, const int b, const int lane,
     // row order: agent rows, target rows (N*Tper edges), obstacle rows
     int64_t o = off + (incl - cnt) + (lane >= s.N ? s.N * s.Tper : 0);
     auto put = [&](int a_row, float2 a, int d_row) {
-        const float2 q = s_pos[d_row];
-        const float dx = a.x - q.x, dy = a.y - q.y;
-        src[o] = g0 + a_row;
-        dst[o] = g0 + d_row;
-        p.edge_attr[o] = sqrtf(dx * dx + dy * dy);
+        if (o < p.edge_capacity) {   // redirected outputs may be smaller than the worst case
+            const float2 q = s_pos[d_row];
+            const float dx = a.x - q.x, dy = a.y - q.y;
+            src[o] = g0 + a_row;
+            dst[o] = g0 + d_row;
+            p.edge_attr[o] = sqrtf(dx * dx + dy * dy);
+        }
         ++o;
     };
     if (lane < s.M) {

@@ -257,44 +257,40 @@ __device__ __forceinline__ void emit_rows(const DevParams &p, const Shape<kN, kN
     if (!L.live) return;
 
     const float2 pm = s_pos[row_entity(m, N)];
-    int32_t *src = p.edge_index, *dst = p.edge_index + p.edge_capacity;
+    const int64_t cap = p.edge_capacity;   // redirected outputs may be smaller than the worst case
+    int32_t *src = p.edge_index, *dst = p.edge_index + cap;
     float *attr = p.edge_attr;
     const int32_t g0 = (int32_t)(eb * E);
     const int32_t gs = g0 + row_entity(m, N);
     const uint64_t agent_bits = N >= 64 ? ~0ull : ((1ull << N) - 1);
     uint64_t lo = mask & agent_bits, hi = mask & ~agent_bits;
+    auto put = [&](int64_t at, int32_t a, int32_t b, float d) {
+        if (at < cap) {
+            src[at] = a;
+            dst[at] = b;
+            attr[at] = d;
+        }
+    };
     while (lo) {
         const int j = __builtin_ctzll(lo);
         lo &= lo - 1;
         const float2 q = s_pos[j];
         const float dx = pm.x - q.x, dy = pm.y - q.y;
-        src[o] = gs;
-        dst[o] = g0 + j;
-        attr[o] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-        ++o;
+        put(o++, gs, g0 + j, __builtin_amdgcn_sqrtf(dx * dx + dy * dy));
     }
     if (L.agent) {
         const float2 g = s_pos[N + m];
         const float dx = pm.x - g.x, dy = pm.y - g.y;
         const float d = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-        src[o] = gs;                    // agent m -> its goal
-        dst[o] = g0 + N + m;
-        attr[o] = d;
-        ++o;
-        const int64_t og = env_off + a_total + m;
-        src[og] = g0 + N + m;           // goal row: goal m -> agent m
-        dst[og] = gs;
-        attr[og] = d;
+        put(o++, gs, g0 + N + m, d);                  // agent m -> its goal
+        put(env_off + a_total + m, g0 + N + m, gs, d);  // goal row: goal m -> agent m
     }
     while (hi) {
         const int j = __builtin_ctzll(hi);
         hi &= hi - 1;
         const float2 q = s_pos[N + j];
         const float dx = pm.x - q.x, dy = pm.y - q.y;
-        src[o] = gs;
-        dst[o] = g0 + N + j;
-        attr[o] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-        ++o;
+        put(o++, gs, g0 + N + j, __builtin_amdgcn_sqrtf(dx * dx + dy * dy));
     }
 }
 
@@ -494,7 +490,7 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
     // ---- outputs and state. Node features: agent rows every step; goal and
     // obstacle rows (static within an episode) only when the layout is new or
     // on an observe. Rows are staged in LDS and stored lane-linear.
-    const bool any_statics = p.mode != kModeStep || __any(relaid);
+    const bool any_statics = p.mode != kModeStep || p.nf_full || __any(relaid);
     if (L.live) {
         float *nf = s_nf + segc * E * 7;
         if (L.agent) {
@@ -520,7 +516,7 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
         for (int g = 0; g < G; ++g) {
             if (b0 + g >= p.B) break;
             // per env, not per lane: idle lanes of the env's wave copy too
-            const bool full_rows = p.mode != kModeStep || (kG == 1 ? __any(relaid) : __shfl(relaid, g * M));
+            const bool full_rows = p.mode != kModeStep || p.nf_full || (kG == 1 ? __any(relaid) : __shfl(relaid, g * M));
             const int len = (full_rows ? E : N) * 7;
             float *dst = p.node_feat + (int64_t)(b0 + g) * E * 7;
             const float *src = s_nf + g * E * 7;

@@ -315,7 +315,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
     // node features [E][7] = [vx vy px py gx-px gy-py type]: agent rows every
     // step (one thread per row), goal/obstacle rows only on layout change
     float *nf = p.node_feat + eb * E * 7;
-    const bool full = p.mode != kModeStep || relaid;
+    const bool full = p.mode != kModeStep || relaid || p.nf_full;
 #ifdef GSM_ABL_NO_NF
     if (!full) goto skip_nf;
 #endif
@@ -374,7 +374,7 @@ __device__ __forceinline__ int row_edges(const DevParams &p, const float2 *s_pos
                                          int64_t off, int32_t g0) {
     const int N = p.N, W = p.W;
     if (r >= N && r < 2 * N) {   // goal row: goal i -> agent i
-        if (kWrite) {
+        if (kWrite && off < p.edge_capacity) {
             const float2 a = s_pos[r], q = s_pos[r - N];
             const float dx = a.x - q.x, dy = a.y - q.y;
             p.edge_index[off] = g0 + r;
@@ -393,11 +393,13 @@ __device__ __forceinline__ int row_edges(const DevParams &p, const float2 *s_pos
     const float2 a = s_pos[r];
     int n = 0;
     auto put = [&](int dst) {
-        const float2 q = s_pos[dst];
-        const float dx = a.x - q.x, dy = a.y - q.y;
-        p.edge_index[off + n] = g0 + r;
-        p.edge_index[p.edge_capacity + off + n] = g0 + dst;
-        p.edge_attr[off + n] = sqrtf(dx * dx + dy * dy);
+        if (off + n < p.edge_capacity) {   // redirected outputs may be smaller than the worst case
+            const float2 q = s_pos[dst];
+            const float dx = a.x - q.x, dy = a.y - q.y;
+            p.edge_index[off + n] = g0 + r;
+            p.edge_index[p.edge_capacity + off + n] = g0 + dst;
+            p.edge_attr[off + n] = sqrtf(dx * dx + dy * dy);
+        }
         ++n;
     };
     bool goal_done = r >= N;

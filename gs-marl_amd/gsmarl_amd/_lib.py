@@ -52,6 +52,14 @@ class GsmBuffers(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in BUFFER_FIELDS]
 
 
+OUTPUT_FIELDS = ["node_feat", "reward", "cost", "done", "edge_count", "edge_ptr", "edge_index", "edge_attr",
+                 "assign"]
+
+
+class GsmOutputs(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in OUTPUT_FIELDS] + [("edge_capacity", C.c_int64)]
+
+
 # every symbol include/gsm.h declares, with its ctypes signature
 _P = C.c_void_p
 SIGNATURES = {
@@ -62,6 +70,10 @@ SIGNATURES = {
     "gsm_reset": (C.c_int, [_P, C.c_uint64, C.c_int, _P, _P]),
     "gsm_step": (C.c_int, [_P, _P, C.c_int, _P]),
     "gsm_observe": (C.c_int, [_P, _P]),
+    "gsm_step_into": (C.c_int, [_P, _P, C.c_int, C.POINTER(GsmOutputs), _P]),
+    "gsm_observe_into": (C.c_int, [_P, C.POINTER(GsmOutputs), _P]),
+    "gsm_graph_capture_into": (C.c_int, [_P, C.c_int32, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int,
+                                         C.POINTER(GsmOutputs)]),
     "gsm_graph_capture": (C.c_int, [_P, C.c_int32, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int, C.c_int]),
     "gsm_graph_launch": (C.c_int, [_P, C.c_int32, _P]),
     "gsm_graph_kernel_ms": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_float),

@@ -147,17 +147,52 @@ class GpuBatchEnv:
         raise ValueError(f"actions must be int32 [B,N], float32 one-hot [B,N,5] or float32 [B,N,2]; "
                          f"got {actions.dtype} {tuple(actions.shape)}")
 
-    def step(self, actions: torch.Tensor, sync_edges: bool = True) -> dict:
+    def _outputs_struct(self, out: dict) -> "_lib.GsmOutputs":
+        """gsm_outputs for a dict of device tensors (missing keys keep the
+        bound buffers). Shapes must match the bound outputs; edge arrays may be
+        smaller than the worst case (edge_index [2, cap], edge_attr [cap])."""
+        o = _lib.GsmOutputs()
+        for k, v in out.items():
+            if k not in _lib.OUTPUT_FIELDS:
+                raise KeyError(f"not a redirectable output: {k}")
+            ref = self.t[k]
+            if v.device != self.device or v.dtype != ref.dtype or not v.is_contiguous():
+                raise ValueError(f"output {k}: need a contiguous {ref.dtype} tensor on {self.device}")
+            if k in ("edge_index", "edge_attr"):
+                continue
+            if v.shape != ref.shape:
+                raise ValueError(f"output {k}: shape {tuple(v.shape)} != {tuple(ref.shape)}")
+            setattr(o, k, v.data_ptr())
+        if ("edge_index" in out) != ("edge_attr" in out):
+            raise ValueError("edge_index and edge_attr are redirected together")
+        if "edge_index" in out:
+            ei, ea = out["edge_index"], out["edge_attr"]
+            if ei.dim() != 2 or ei.shape[0] != 2 or ea.shape != (ei.shape[1],):
+                raise ValueError("edge_index must be [2, cap] and edge_attr [cap]")
+            o.edge_index, o.edge_attr, o.edge_capacity = ei.data_ptr(), ea.data_ptr(), int(ei.shape[1])
+        return o
+
+    def step(self, actions: torch.Tensor, sync_edges: bool = True, out: Optional[dict] = None) -> dict:
+        """One env.step. With ``out`` (a dict of device tensors, e.g. a rollout
+        buffer slot) the step writes those outputs there instead (no copies)."""
         if not actions.is_contiguous():
             actions = actions.contiguous()
         fmt = self._action_fmt(actions)
-        self._chk(self.lib.gsm_step(self._h, C.c_void_p(actions.data_ptr()), fmt, self._stream()),
-                  "gsm_step")
-        return self.outputs(sync_edges)
+        a = C.c_void_p(actions.data_ptr())
+        if out is None:
+            self._chk(self.lib.gsm_step(self._h, a, fmt, self._stream()), "gsm_step")
+            return self.outputs(sync_edges)
+        o = self._outputs_struct(out)
+        self._chk(self.lib.gsm_step_into(self._h, a, fmt, C.byref(o), self._stream()), "gsm_step_into")
+        return out
 
-    def observe(self, sync_edges: bool = True) -> dict:
-        self._chk(self.lib.gsm_observe(self._h, self._stream()), "gsm_observe")
-        return self.outputs(sync_edges)
+    def observe(self, sync_edges: bool = True, out: Optional[dict] = None) -> dict:
+        if out is None:
+            self._chk(self.lib.gsm_observe(self._h, self._stream()), "gsm_observe")
+            return self.outputs(sync_edges)
+        o = self._outputs_struct(out)
+        self._chk(self.lib.gsm_observe_into(self._h, C.byref(o), self._stream()), "gsm_observe_into")
+        return out
 
     # ------------------------------------------------- checkpoint / injection
     STATE_KEYS = ("pos", "vel", "step_count", "episode", "ep_acc", "ep_last")
@@ -197,6 +232,17 @@ class GpuBatchEnv:
         self._graph_actions[slot] = a   # keep alive while the graph exists
         self._chk(self.lib.gsm_graph_capture(self._h, int(slot), ptr, stride, n_act, int(n_steps), fmt,
                                              flags), "gsm_graph_capture")
+
+    def capture_into(self, actions_seq: torch.Tensor, outs: list, slot: int = 0) -> None:
+        """HIP graph of len(outs) steps; the j-th step uses actions_seq[j %
+        len(actions_seq)] and writes its outputs to outs[j] (dicts as in step)."""
+        a = actions_seq.contiguous()
+        fmt = self._action_fmt(a[0])
+        stride = a[0].numel() * a.element_size()
+        arr = (_lib.GsmOutputs * len(outs))(*[self._outputs_struct(o) for o in outs])
+        self._graph_actions[slot] = (a, outs)   # keep alive while the graph exists
+        self._chk(self.lib.gsm_graph_capture_into(self._h, int(slot), C.c_void_p(a.data_ptr()), stride,
+                                                  a.shape[0], len(outs), fmt, arr), "gsm_graph_capture_into")
 
     def replay(self, slot: int = 0) -> None:
         self._chk(self.lib.gsm_graph_launch(self._h, int(slot), self._stream()), "gsm_graph_launch")

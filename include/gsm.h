@@ -134,6 +134,26 @@ typedef struct gsm_buffers {
     int32_t *assign;          /* [B][N] polygon/line slot of each agent (LSA), -1 else */
 } gsm_buffers;
 
+/* Output redirection (an on-device rollout buffer
+ * filled without copies). Where one step / observe writes its outputs; NULL
+ * members keep the bound buffers. edge_index is [2][edge_capacity] when
+ * redirected; edges past edge_capacity are not written, while edge_ptr keeps
+ * the true offsets (edge_ptr[B] > edge_capacity flags the overflow). A
+ * redirected launch writes full node-feature rows (goal / obstacle rows are
+ * otherwise rewritten only when a layout changes). */
+typedef struct gsm_outputs {
+    float *node_feat;         /* [B][E][7] */
+    float *reward;            /* [B][N]    */
+    float *cost;              /* [B][N]    */
+    uint8_t *done;            /* [B]       */
+    int32_t *edge_count;      /* [B]       */
+    int64_t *edge_ptr;        /* [B+1]     */
+    int32_t *edge_index;      /* [2][edge_capacity] */
+    float *edge_attr;         /* [edge_capacity]    */
+    int32_t *assign;          /* [B][N]  (ragged scenarios) */
+    int64_t edge_capacity;
+} gsm_outputs;
+
 typedef struct gsm_handle gsm_handle;
 
 int gsm_abi_version(void);
@@ -163,6 +183,10 @@ int gsm_step(gsm_handle *h, const void *actions, int action_fmt, void *stream);
  * state buffers, e.g. set_state). */
 int gsm_observe(gsm_handle *h, void *stream);
 
+/* gsm_step / gsm_observe with their outputs redirected (gsm_outputs). */
+int gsm_step_into(gsm_handle *h, const void *actions, int action_fmt, const gsm_outputs *out, void *stream);
+int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream);
+
 /* Build HIP graph `slot` (0..GSM_GRAPH_SLOTS-1) of n_steps steps; the j-th
  * step reads its actions at actions + (j % n_actions) * action_stride_bytes.
  * flags: which kernels each step runs (GSM_GRAPH_STEP | GSM_GRAPH_EMIT; 0 =
@@ -178,6 +202,10 @@ int gsm_observe(gsm_handle *h, void *stream);
 #define GSM_GRAPH_TIME_ENDS 8
 int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t action_stride_bytes,
                       int32_t n_actions, int32_t n_steps, int action_fmt, int flags);
+/* As gsm_graph_capture (both kernels, no timing events), with the j-th
+ * step's outputs redirected to per_step[j] (n_steps entries). */
+int gsm_graph_capture_into(gsm_handle *h, int32_t slot, const void *actions, int64_t action_stride_bytes,
+                           int32_t n_actions, int32_t n_steps, int action_fmt, const gsm_outputs *per_step);
 int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream);
 /* After a timed launch of `slot` has completed: mean duration (ms) of the
  * step and emit kernels (TIME_EACH), and the whole graph (both flags). */

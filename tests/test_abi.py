@@ -50,8 +50,10 @@ def test_struct_layouts_match_header(lib, tmp_path):
     fields_cfg = [f for f, _ in _lib.GsmConfig._fields_]
     fields_buf = [f for f, _ in _lib.GsmBuffers._fields_]
     fields_sz = [f for f, _ in _lib.GsmSizes._fields_]
+    fields_out = [f for f, _ in _lib.GsmOutputs._fields_]
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gsm.h"', "int main(void){"]
-    for s, fs in (("gsm_config", fields_cfg), ("gsm_buffers", fields_buf), ("gsm_sizes", fields_sz)):
+    for s, fs in (("gsm_config", fields_cfg), ("gsm_buffers", fields_buf), ("gsm_sizes", fields_sz),
+                  ("gsm_outputs", fields_out)):
         lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
         for f in fs:
             lines.append(f'printf("{s}.{f} %zu\\n", offsetof({s}, {f}));')
@@ -61,7 +63,8 @@ def test_struct_layouts_match_header(lib, tmp_path):
     subprocess.run(["gcc", "-I", str(ROOT / "include"), str(probe), "-o", str(exe)], check=True)
     got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True,
                                                          check=True).stdout.split("\n") if l)
-    for s, cls in (("gsm_config", _lib.GsmConfig), ("gsm_buffers", _lib.GsmBuffers), ("gsm_sizes", _lib.GsmSizes)):
+    for s, cls in (("gsm_config", _lib.GsmConfig), ("gsm_buffers", _lib.GsmBuffers), ("gsm_sizes", _lib.GsmSizes),
+                   ("gsm_outputs", _lib.GsmOutputs)):
         assert int(got[s]) == C.sizeof(cls), s
         for f, _ in cls._fields_:
             assert int(got[f"{s}.{f}"]) == getattr(cls, f).offset, f"{s}.{f}"
