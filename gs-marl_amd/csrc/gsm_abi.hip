@@ -449,7 +449,7 @@ static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_
         hipKernelNodeParams kp = {};
         void *args[] = {&p};
         kp.func = const_cast<void *>(fn);
-        kp.gridDim = dim3(gsm::grid_blocks(p));
+        kp.gridDim = dim3(fn == gsm::step_kernel_fn(p) ? gsm::step_grid_blocks(p) : gsm::grid_blocks(p));
         kp.blockDim = dim3(gsm::block_threads(p));
         kp.sharedMemBytes = (unsigned)lds;
         kp.kernelParams = args;

@@ -62,7 +62,8 @@ struct DevParams {
 // emitter for all B envs on `s`. Returns the first hipError_t.
 hipError_t launch_step(const DevParams &p, hipStream_t s);
 // for explicit graph construction (kernel nodes)
-int grid_blocks(const DevParams &p);
+int grid_blocks(const DevParams &p);        // emit kernel (and tile/ragged step) workgroups
+int step_grid_blocks(const DevParams &p);   // step kernel workgroups
 const void *step_kernel_fn(const DevParams &p);
 const void *emit_kernel_fn(const DevParams &p);
 const void *step_seg_kernel_fn(const DevParams &p);

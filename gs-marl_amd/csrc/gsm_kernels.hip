@@ -25,6 +25,7 @@ int grid_blocks(const DevParams &p) {
     const int per_block = kWavesPerBlock * p.G;
     return (p.B + per_block - 1) / per_block;
 }
+int step_grid_blocks(const DevParams &p) { return grid_blocks(p); }
 const void *step_kernel_fn(const DevParams &p) {
     if (p.path == kPathRagged) return step_ragged_kernel_fn();
     if (p.path == kPathTile) return step_tile_kernel_fn();
@@ -42,19 +43,19 @@ size_t emit_kernel_lds(const DevParams &p) {
     return p.path == kPathTile ? (size_t)p.wave_lds_emit : (size_t)kWavesPerBlock * p.wave_lds_emit + 16;
 }
 
-static hipError_t launch_fn(const void *fn, const DevParams &p, size_t lds, hipStream_t s) {
+static hipError_t launch_fn(const void *fn, const DevParams &p, int grid, size_t lds, hipStream_t s) {
     (void)hipGetLastError();   // report this launch's error only
     void *args[] = {const_cast<DevParams *>(&p)};
-    const hipError_t e = hipLaunchKernel(fn, dim3(grid_blocks(p)), dim3(block_threads(p)), args, lds, s);
+    const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(block_threads(p)), args, lds, s);
     return e != hipSuccess ? e : hipGetLastError();
 }
 
 hipError_t launch_step_kernel(const DevParams &p, hipStream_t s) {
-    return launch_fn(step_kernel_fn(p), p, step_kernel_lds(p), s);
+    return launch_fn(step_kernel_fn(p), p, step_grid_blocks(p), step_kernel_lds(p), s);
 }
 
 hipError_t launch_emit_kernel(const DevParams &p, hipStream_t s) {
-    return launch_fn(emit_kernel_fn(p), p, emit_kernel_lds(p), s);
+    return launch_fn(emit_kernel_fn(p), p, grid_blocks(p), emit_kernel_lds(p), s);
 }
 
 hipError_t launch_step(const DevParams &p, hipStream_t s) {

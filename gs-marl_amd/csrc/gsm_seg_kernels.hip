@@ -302,17 +302,55 @@ __device__ __forceinline__ void emit_rows(const DevParams &p, const Shape<kN, kN
 #else
 #define GSM_STEP_ATTR
 #endif
+// Global inputs of one env for a one-env-per-wave (G = 1) wave, loaded into
+// registers before the first wait. (Processing two envs per wave in turn with
+// the second's loads in flight measured slower: DESIGN.md §8.)
+struct SegIn {
+    float2 x0, x1, v, u;
+    uint64_t cand_prev, oo;
+    int t, ep;
+    float2 acc;
+};
+
 template <int kN, int kNo, int kFmt>
-__global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevParams p) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const Shape<kN, kNo> s(p);
+__device__ __forceinline__ SegIn seg_load(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L) {
+    SegIn in;
+    in.x0 = in.x1 = in.v = in.u = make_float2(0.0f, 0.0f);
+    in.cand_prev = in.oo = 0;
+    in.t = in.ep = 0;
+    in.acc = make_float2(0.0f, 0.0f);
+    const int N = s.N, E = s.E, M = s.M;
+    if (L.b < p.B) {
+        const int64_t eb = L.b;
+        const uint32_t um = (uint32_t)L.m;
+        const float2 *pos_b = p.pos + eb * E;
+        if (L.lane < E) in.x0 = pos_b[(uint32_t)L.lane];
+        if (L.lane + kWave < E) in.x1 = pos_b[(uint32_t)(L.lane + kWave)];
+        in.t = p.step_count[L.b];
+        in.ep = p.episode[L.b];
+        in.acc = p.ep_acc[L.b];
+        if (L.agent) {
+            in.v = (p.vel + eb * N)[um];
+            if (p.mode == kModeStep) {
+                in.u = action_force_t<kFmt>(p, eb * N + um);
+                in.cand_prev = (p.contact_mask + eb * N)[um];
+            }
+        }
+        if (L.live && L.m >= N && p.mode == kModeStep) in.oo = (p.row_mask + eb * M)[um];
+    }
+    return in;
+}
+
+// One env (G = 1) or one wave's G envs: everything after the loads. Returns
+// the wave's edge count (the sum over its envs).
+template <int kN, int kNo, int kFmt>
+__device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L,
+                                       unsigned char *wave_lds, const SegIn &in, int64_t wid) {
     constexpr int kG = envs_per_wave<kN, kNo>();
-    const Lane L = seg_lane(p, s);
     const int N = s.N, E = s.E, M = s.M, G = s.G;
-    const int wave = L.wave;
     const int segc = L.seg < G ? L.seg : G - 1;             // clamp idle lanes' addresses
-    float2 *s_pos = (float2 *)(smem + wave * p.wave_lds_step) + segc * E;
-    float *s_nf = (float *)((float2 *)(smem + wave * p.wave_lds_step) + G * E);   // [G][E][7]
+    float2 *s_pos = (float2 *)wave_lds + segc * E;
+    float *s_nf = (float *)((float2 *)wave_lds + G * E);    // [G][E][7]
     const int m = L.m;
     const bool obst = L.live && m >= N;
     const bool wave_live = kG == 1 ? L.b < p.B : true;
@@ -322,33 +360,16 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
     float2 *const pos_b = p.pos + eb * E;
     float2 *const vel_b = p.vel + eb * N;
     const uint32_t um = (uint32_t)m;
-    const int64_t wid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-    GSM_RSTAMP(p, wid, 8);
-    GSM_STAMP(p, wid, 0);
+    (void)wid;
 
-    // ---- load: issue every global load before the first wait
-    int t = 0, ep = 0;
-    float2 acc = make_float2(0.0f, 0.0f);
-    float2 v = make_float2(0.0f, 0.0f), u = make_float2(0.0f, 0.0f);
-    uint64_t cand_prev = 0, oo = 0;
+    int t = in.t, ep = in.ep;
+    float2 acc = in.acc;
+    float2 v = in.v, u = in.u;
+    uint64_t cand_prev = in.cand_prev, oo = in.oo;
     if constexpr (kG == 1) {
         if (wave_live) {
-            float2 x0 = make_float2(0.0f, 0.0f), x1 = x0;
-            if (L.lane < E) x0 = pos_b[(uint32_t)L.lane];
-            if (L.lane + kWave < E) x1 = pos_b[(uint32_t)(L.lane + kWave)];
-            t = p.step_count[L.b];
-            ep = p.episode[L.b];
-            acc = p.ep_acc[L.b];
-            if (L.agent) {
-                v = vel_b[um];
-                if (p.mode == kModeStep) {
-                    u = action_force_t<kFmt>(p, eb * N + um);
-                    cand_prev = (p.contact_mask + eb * N)[um];
-                }
-            }
-            if (obst && p.mode == kModeStep) oo = (p.row_mask + eb * M)[um];
-            if (L.lane < E) s_pos[L.lane] = x0;
-            if (L.lane + kWave < E) s_pos[L.lane + kWave] = x1;
+            if (L.lane < E) s_pos[L.lane] = in.x0;
+            if (L.lane + kWave < E) s_pos[L.lane + kWave] = in.x1;
         }
     } else {
         if (L.live) {
@@ -368,7 +389,6 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
     }
     bool reset = L.live && p.mode == kModeReset && (p.env_mask == nullptr || p.env_mask[L.b] != 0);
     wave_sync();
-    GSM_STAMP(p, wid, 1);
 
     // scenario.reset_world (Philox layout, App. A S14) for the lanes' envs
     auto relayout = [&]() {
@@ -427,7 +447,6 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
         done = L.live && t >= p.EL;
     }
 
-    GSM_STAMP(p, wid, 2);
     // ---- observation pass on the post-physics positions
     const bool full = p.mode != kModeStep;                  // reset / observe: recompute obstacle pairs
     float2 pm = s_pos[row_entity(m, N)];
@@ -440,7 +459,6 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
     obs_sweep<kN, kNo, kG>(p, s, L, s_pos, pm, full, oo, row, cand, ccnt);
 #endif
 
-    GSM_STAMP(p, wid, 3);
     // reward / cost callbacks
     float r = 0.0f;
     if (L.agent) {
@@ -448,16 +466,13 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
         const float dx = pm.x - g.x, dy = pm.y - g.y;
         r = -__builtin_amdgcn_sqrtf(dx * dx + dy * dy);
     }
-    GSM_STAMP(p, wid, 10);
     float rsum = seg_total<kG>(r, L, M);
     const int ci = L.agent ? ccnt : 0;
     const int csum = seg_total<kG>(ci, L, M);
-    GSM_STAMP(p, wid, 11);
     if (L.agent) {
         (p.reward + eb * N)[um] = p.shared_reward ? rsum : r;
         (p.cost + eb * N)[um] = (float)ci;
     }
-    GSM_STAMP(p, wid, 12);
     if (p.shared_reward) rsum *= (float)N;
     bool relaid = reset;                                    // layout changed in this launch
     if (p.mode == kModeStep) {
@@ -485,7 +500,6 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
         }
     }
     if (!L.live) row = 0;
-    GSM_STAMP(p, wid, 4);
 
     // ---- outputs and state. Node features: agent rows every step; goal and
     // obstacle rows (static within an episode) only when the layout is new or
@@ -512,7 +526,7 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
     }
     wave_sync();
     {
-        const int b0 = kG == 1 ? L.b : (blockIdx.x * kWavesPerBlock + wave) * G;
+        const int b0 = kG == 1 ? L.b : (blockIdx.x * kWavesPerBlock + L.wave) * G;
         for (int g = 0; g < G; ++g) {
             if (b0 + g >= p.B) break;
             // per env, not per lane: idle lanes of the env's wave copy too
@@ -530,7 +544,6 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
 #ifdef GSM_ABL_FUSED_PADDED   // timing-only: emit here at a fixed per-env stride
     emit_rows<kN, kNo, kG>(p, s, L, s_pos, row, (int64_t)(L.live ? L.b : 0) * (p.edge_capacity / p.B));
 #endif
-    GSM_STAMP(p, wid, 5);
     // edge count (radius rows + goal edges both ways)
     const int edges = __popcll(row) + ((L.live && m == 0) ? 2 * N : 0);
     int wave_edges;
@@ -554,16 +567,32 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
             p.edge_count[L.b] = env_edges;
         }
     }
+    return wave_edges;
+}
+
+template <int kN, int kNo, int kFmt>
+__global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const Shape<kN, kNo> s(p);
+    constexpr int kG = envs_per_wave<kN, kNo>();
+    const Lane L = seg_lane(p, s);
+    const int wave = L.wave;
+    unsigned char *wave_lds = smem + wave * p.wave_lds_step;
+    const int64_t wid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
     int *s_bc = (int *)(smem + kWavesPerBlock * p.wave_lds_step);
-    if (L.lane == 0) s_bc[wave] = wave_edges;
-    GSM_STAMP(p, wid, 6);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        int q = 0;
-        for (int k = 0; k < kWavesPerBlock; ++k) q += s_bc[k];
-        p.block_edge_sum[blockIdx.x] = q;
+    GSM_RSTAMP(p, wid, 8);
+    {
+        SegIn in{};
+        if constexpr (kG == 1) in = seg_load<kN, kNo, kFmt>(p, s, L);
+        const int edges = seg_env<kN, kNo, kFmt>(p, s, L, wave_lds, in, wid);
+        if (L.lane == 0) s_bc[wave] = edges;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int q = 0;
+            for (int k = 0; k < kWavesPerBlock; ++k) q += s_bc[k];
+            p.block_edge_sum[blockIdx.x] = q;
+        }
     }
-    GSM_STAMP(p, wid, 7);
     GSM_RSTAMP(p, wid, 9);
 }
 
@@ -574,7 +603,7 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
     const Shape<kN, kNo> s(p);
     constexpr int kG = envs_per_wave<kN, kNo>();
     const Lane L = seg_lane(p, s);
-    const int N = s.N, E = s.E, M = s.M, G = s.G;
+    const int E = s.E, M = s.M, G = s.G;
     const int wave = L.wave;
     const int segc = L.seg < G ? L.seg : G - 1;
     float2 *s_pos = (float2 *)(smem + wave * p.wave_lds_emit) + segc * E;
