@@ -109,52 +109,85 @@ CONFIGS = {   # BASELINE.json configs runnable as a one-GPU bench line
 }
 
 
-def cpu_baseline_ragged(cfg, seconds):
-    """Ragged restatement (oracle/ragged_ref.py, per-env NumPy + the scipy-
-    equivalent LSA restatement) on one host core, over a 30-env sample."""
+def _cpu_worker(job):
+    """One host process: step one CPU restatement for `seconds`; returns
+    (agent-steps, elapsed). kind "nav": oracle/mpe_ref.py (object-per-entity
+    MPE, Python pair loop, fp64), one env; kind "ragged": oracle/ragged_ref.py
+    over a 30-env mixed sample (per-env NumPy + the assignment restatement)."""
+    kind, cfgd, seconds, seed = job
     import numpy as np
-    from oracle import ragged_ref as rr
-    keys = set(rr.br.DEFAULTS) | set(rr.RAGGED_DEFAULTS)
-    rcfg = rr.make_cfg(**{k: v for k, v in cfg.to_dict().items() if k in keys})
-    rcfg.n_envs = 30
-    st = rr.new_state(rcfg)
-    rng = np.random.default_rng(0)
-    agents = int(st["n"].sum())
-    steps = 0
-    t0 = time.perf_counter()
-    while True:
-        st, _ = rr.step(rcfg, st, rng.integers(0, 5, (30, cfg.n_agents)), 1, np.float64)
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return dict(value=steps * agents / el, unit="agent-steps/s", cores=1, kind="port",
-                sample=f"30 envs ({agents} agents) x {steps} steps ({el:.1f} s) of oracle/ragged_ref.py step "
-                       f"(per-env NumPy, fp64, per-step assignment via oracle/lsa_ref.py), 1 host core")
+    sys.path.insert(0, str(ROOT))
+    rng = np.random.default_rng(seed)
+    steps, agents = 0, 0
+    if kind == "nav":
+        from oracle import mpe_ref
+        from oracle.batch_ref import make_cfg
+        n = cfgd["n_agents"]
+        env = mpe_ref.GraphConstrainEnv(make_cfg(n_agents=n, seed=seed))
+        env.reset(seed=seed)
+        eye = np.eye(5)
+        agents = n
+        t0 = time.perf_counter()
+        while True:
+            env.step(list(eye[rng.integers(0, 5, size=n)]))
+            steps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    else:
+        from oracle import ragged_ref as rr
+        keys = set(rr.br.DEFAULTS) | set(rr.RAGGED_DEFAULTS)
+        rcfg = rr.make_cfg(**{k: v for k, v in cfgd.items() if k in keys})
+        rcfg.n_envs, rcfg.env_base = 30, 30 * seed
+        st = rr.new_state(rcfg)
+        agents = int(st["n"].sum())
+        t0 = time.perf_counter()
+        while True:
+            st, _ = rr.step(rcfg, st, rng.integers(0, 5, (30, cfgd["n_agents"])), 1, np.float64)
+            steps += 1
+            el = time.perf_counter() - t0
+            if el >= seconds:
+                break
+    return steps * agents, el
 
 
-def cpu_baseline(n_agents, seconds):
-    """Reference-structure CPU restatement (object-per-entity MPE, fp64,
-    Python pair loop: oracle/mpe_ref.py) on one host core."""
-    import numpy as np
-    from oracle import mpe_ref
-    from oracle.batch_ref import make_cfg
-    env = mpe_ref.GraphConstrainEnv(make_cfg(n_agents=n_agents))
-    env.reset(seed=0)
-    rng = np.random.default_rng(0)
-    eye = np.eye(5)
-    steps = 0
-    t0 = time.perf_counter()
-    while True:
-        env.step(list(eye[rng.integers(0, 5, size=n_agents)]))
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return dict(value=steps * n_agents / el, unit="agent-steps/s", cores=1, kind="port",
-                sample=f"1 env x {steps} steps ({el:.1f} s) of oracle/mpe_ref.py GraphConstrainEnv.step "
-                       f"(object-per-entity MPE restatement, fp64, Python pair loop), N={n_agents}, "
-                       f"1 host core; the reference's own CPU path is absent (readme.md:1)")
+def cpu_baseline(cfg, seconds, cores):
+    """The CPU restatement of the reference path timed on `cores` host
+    processes (one env or env sample per process, like the reference's
+    subprocess vec-env); the reference's own CPU path is absent
+    (readme.md:1), so this is a port. Returns the all-core rate and the mean
+    single-process rate."""
+    import multiprocessing as mp
+    kind = "ragged" if cfg.ragged else "nav"
+    cfgd = cfg.to_dict()
+    jobs = [(kind, cfgd, seconds, 1000 + i) for i in range(cores)]
+    if cores == 1:
+        res = [_cpu_worker(jobs[0])]
+    else:
+        # spawned children: fresh interpreters that never touch the GPU
+        with mp.get_context("spawn").Pool(cores) as pool:
+            res = pool.map(_cpu_worker, jobs)
+    total = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    single = sum(r[0] / r[1] for r in res) / len(res)
+    what = ("oracle/mpe_ref.py GraphConstrainEnv.step (object-per-entity MPE restatement, fp64, Python "
+            f"pair loop), N={cfg.n_agents}, one env per process") if kind == "nav" else (
+            "oracle/ragged_ref.py step over a 30-env mixed sample per process (per-env NumPy, fp64, "
+            "assignment via oracle/lsa_ref.py)")
+    return dict(value=total / wall, unit="agent-steps/s", cores=cores, kind="port",
+                single_core_value=single,
+                sample=f"{cores} host processes x {seconds:.0f} s of {what}; the reference's own CPU path is "
+                       f"absent (readme.md:1)")
+
+
+def host_cores():
+    """The host-core share of this job: the affinity set, capped at 16 (the
+    GPU box's share per GPU; nproc shows the whole machine there)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
 
 
 def pmc_traffic(key):
@@ -181,7 +214,8 @@ def main():
     ap.add_argument("--n-envs", type=int, default=None, help="override the config's envs per GPU")
     ap.add_argument("--kernel-launches", type=int, default=100,
                     help="back-to-back launches per kernel for the event-timed roofline")
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-cores", type=int, default=0, help="host processes for the CPU baseline (0: all, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the roofline timing (null)")
     ap.add_argument("--eager", action="store_true", help="launch steps eagerly instead of HIP graphs")
@@ -313,7 +347,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline_ragged(cfg, args.cpu_seconds) if cfg.ragged else cpu_baseline(N, args.cpu_seconds)
+        cpu = cpu_baseline(cfg, args.cpu_seconds, args.cpu_cores or host_cores())
 
     if rank == 0:
         line = {
