@@ -542,6 +542,21 @@ int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_ms, float *emit
     return GSM_OK;
 }
 
+int gsm_attn_aggregate(const float *q, const float *k, const float *v, const float *edge_w, const float *w_e,
+                       const int64_t *row_ptr, const int32_t *col, const float *skip, int64_t n_nodes,
+                       int32_t heads, int32_t channels, float scale, float *out, void *stream) {
+    if (n_nodes < 0 || n_nodes >= ((int64_t)1 << 40)) return fail(nullptr, GSM_EINVAL, "bad n_nodes");
+    if (heads < 1 || channels < 1 || (channels & (channels - 1)) || heads * channels > 64)
+        return fail(nullptr, GSM_EINVAL, "need channels a power of two and heads*channels <= 64");
+    if (n_nodes == 0) return GSM_OK;
+    if (!q || !k || !v || !row_ptr || !col || !out) return fail(nullptr, GSM_EINVAL, "a required pointer is NULL");
+    if (!!edge_w != !!w_e) return fail(nullptr, GSM_EINVAL, "edge_w and w_e go together");
+    const hipError_t e = gsm::launch_attn_aggregate(q, k, v, edge_w, w_e, row_ptr, col, skip, n_nodes,
+                                                    heads * channels, channels, scale, out, as_stream(stream));
+    if (e != hipSuccess) return hip_fail(nullptr, e, "gsm_attn_aggregate launch");
+    return GSM_OK;
+}
+
 int gsm_debug_set_stamps(gsm_handle *h, void *stamps) {
     if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
     h->dp.stamps = (uint64_t *)stamps;

@@ -80,5 +80,9 @@ size_t step_kernel_lds(const DevParams &p);
 size_t emit_kernel_lds(const DevParams &p);
 hipError_t launch_step_kernel(const DevParams &p, hipStream_t s);
 hipError_t launch_emit_kernel(const DevParams &p, hipStream_t s);
+hipError_t launch_attn_aggregate(const float *q, const float *k, const float *v, const float *edge_w,
+                                 const float *w_e, const int64_t *row_ptr, const int32_t *col,
+                                 const float *skip, int64_t n_nodes, int HC, int C, float scale, float *out,
+                                 hipStream_t s);
 
 }  // namespace gsm

@@ -6,10 +6,11 @@ from .environment import MultiAgentConstrainEnv, MultiAgentEnv, MultiAgentGraphC
 from .make_env import make_env
 from .vec_env import GpuGraphVecEnv, make_eval_env, make_train_env
 from .rollout import GraphRolloutBuffer
+from . import gnn
 from . import distributed
 
 __version__ = "0.1.0"
 __all__ = ["EnvConfig", "GpuBatchEnv", "MultiAgentEnv", "MultiAgentConstrainEnv",
            "MultiAgentGraphConstrainEnv", "make_env", "GpuGraphVecEnv", "make_train_env", "make_eval_env",
-           "GraphRolloutBuffer",
+           "GraphRolloutBuffer", "gnn",
            "distributed"]

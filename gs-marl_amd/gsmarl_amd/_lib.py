@@ -78,6 +78,8 @@ SIGNATURES = {
     "gsm_graph_launch": (C.c_int, [_P, C.c_int32, _P]),
     "gsm_graph_kernel_ms": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                       C.POINTER(C.c_float)]),
+    "gsm_attn_aggregate": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_float,
+                                     _P, _P]),
     "gsm_debug_set_stamps": (C.c_int, [_P, _P]),
     "gsm_destroy": (C.c_int, [_P]),
     "gsm_last_error": (C.c_int, [_P, C.c_char_p, C.c_size_t]),

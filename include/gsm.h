@@ -212,6 +212,21 @@ int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream);
 int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_mean_ms, float *emit_mean_ms,
                         float *total_ms);
 
+/* Graph-attention message passing over a CSR graph (SURVEY.md §8(f) next #3:
+ * the GNN encoder after the observation; replaces the edge-softmax /
+ * aggregation of torch-geometric's TransformerConv, requirements.txt:119, as
+ * used by the reference's GNN in gsmarl/algorithms, SOURCES.txt:8). For each
+ * target i with sources j = col[row_ptr[i] .. row_ptr[i+1]), per head h:
+ *   e_ij = edge_w[ij] * w_e[h*C + c]           (edge_w, w_e may be NULL: e = 0)
+ *   a_ij = softmax_j(scale * <q_i[h], k_j[h] + e_ij>)
+ *   out_i[h] = sum_j a_ij (v_j[h] + e_ij) + skip_i[h]      (skip may be NULL)
+ * q, k, v, skip, out: device f32 [n_nodes][heads*channels]; row_ptr: int64
+ * [n_nodes+1]; col: int32 source ids; channels a power of two and
+ * heads*channels <= 64. Stateless; asynchronous on `stream`. */
+int gsm_attn_aggregate(const float *q, const float *k, const float *v, const float *edge_w, const float *w_e,
+                       const int64_t *row_ptr, const int32_t *col, const float *skip, int64_t n_nodes,
+                       int32_t heads, int32_t channels, float scale, float *out, void *stream);
+
 /* Diagnostics: device buffer (uint64 [2 * n_blocks * 4][16]) that libraries
  * built with -DGSM_STAMPS fill with per-wave phase timestamps; ignored by the
  * product build. NULL disables. */
