@@ -7,7 +7,9 @@ owns 8192 envs with global Philox env ids, BASELINE configs[4] at N=8).
 
 A "step" = one env.step of every env on the GPU: action force, pairwise
 contact physics, integration, reward, collision cost, done/auto-reset, node
-features and the packed COO edge list (two kernels). Actions
+features and the packed COO edge list (inside a graph the
+segmented configs run one launch per step — step j+1's kernel first emits
+step j's edges — plus one emit launch at the end of the graph). Actions
 are pre-generated on device (100 x B x N int32, uniform over the 5 discrete
 actions) so the timed region has no host work; the K timed steps are
 replayed from HIP graphs of one episode (100 steps) each, with the per-episode
@@ -74,6 +76,14 @@ def emit_kernel_bytes(B, N, No, total_edges, seg=True):
     E, M = 2 * N + No, N + No
     per_env = 8 * E + 4 + 8 + 8 * M * (1 if seg else (M + 63) // 64)
     return B * per_env + 12 * total_edges
+
+
+def lag_extra_bytes(B, N, No, total_edges):
+    """Bytes a lagged step kernel moves on top of step_kernel_bytes: the
+    previous step's emission minus what the step part already reads (entity
+    positions, obstacle row masks) — the agent row masks, edge count, the
+    edge_ptr entry and 12 B per edge."""
+    return B * (8 * N + 4 + 8) + 12 * total_edges
 
 
 def ragged_kernel_bytes(env, EL, action_bytes, total_edges):
@@ -219,6 +229,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the roofline timing (null)")
     ap.add_argument("--eager", action="store_true", help="launch steps eagerly instead of HIP graphs")
+    ap.add_argument("--unfused", action="store_true",
+                    help="two launches per step in the graphs (no lagged emission)")
     args = ap.parse_args()
 
     import torch
@@ -256,12 +268,13 @@ def main():
     K, W = args.steps, args.warmup
     chunk = min(K, EL)
     n_chunks, rem = divmod(K, chunk)
+    gk = "unfused" if args.unfused else "both"
     if not args.eager:
         if W > 0:
-            env.capture(actions, W, timing=False, slot=2)
-        env.capture(actions, chunk, timing=False, slot=0)
+            env.capture(actions, W, timing=False, slot=2, kernels=gk)
+        env.capture(actions, chunk, timing=False, slot=0, kernels=gk)
         if rem:
-            env.capture(actions, rem, timing=False, slot=1)
+            env.capture(actions, rem, timing=False, slot=1, kernels=gk)
     # warmup
     if W > 0:
         if args.eager:
@@ -297,6 +310,7 @@ def main():
     elapsed = max_over_ranks(elapsed, device=dev) if world > 1 else elapsed
 
     total_edges = int(env.t["edge_ptr"][B].item())
+    seg_cfg = (N + cfg.n_obstacles) <= 64 and not cfg.ragged
     # agents per step on this rank (ragged: sum of N_env), summed over ranks
     agents = int((env.t["env_shape"] & 0xFF).sum().item()) if cfg.ragged else B * N
     if world > 1:
@@ -313,7 +327,8 @@ def main():
     if not args.no_kernel_timing and not args.eager:
         L = args.kernel_launches
         seg = (N + cfg.n_obstacles) <= 64 and not cfg.ragged
-        env.capture(actions, L, slot=3, kernels="step", time_ends=True)
+        lag = seg and not args.unfused
+        env.capture(actions, L, slot=3, kernels="lag" if lag else "step", time_ends=True)
         env.replay(3)
         torch.cuda.synchronize()
         step_ms = env.graph_kernel_ms(3)[0]
@@ -327,17 +342,20 @@ def main():
             names = ("gsm_step_ragged_kernel", "gsm_emit_ragged_kernel")
         else:
             sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4, seg)
+            if lag:
+                sb += lag_extra_bytes(B, N, cfg.n_obstacles, edges_now)
             eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)
-            names = ("gsm_step_seg_kernel", "gsm_emit_seg_kernel") if seg else ("gsm_step_tile_kernel",
-                                                                               "gsm_emit_tile_kernel")
+            names = (("gsm_step_seg_kernel<lagged emission>" if lag else "gsm_step_seg_kernel"),
+                     "gsm_emit_seg_kernel") if seg else ("gsm_step_tile_kernel", "gsm_emit_tile_kernel")
         kern = {"step": dict(kernel=names[0], ms=step_ms, bytes=sb, gbs=sb / (step_ms * 1e-3) / 1e9),
                 "emit": dict(kernel=names[1], ms=emit_ms, bytes=eb, gbs=eb / (emit_ms * 1e-3) / 1e9)}
-        dom = "step" if step_ms >= emit_ms else "emit"
+        # a lagged chain runs the emit kernel once per graph, the step kernel every step
+        dom = "step" if (lag or step_ms >= emit_ms) else "emit"
         k = kern[dom]
         other = kern["emit" if dom == "step" else "step"]
         roofline = dict(kernel=k["kernel"], bound="hbm", achieved=round(k["gbs"], 1), peak=HBM_PEAK_GBS,
                         unit="GB/s", frac=round(k["gbs"] / HBM_PEAK_GBS, 4),
-                        traffic=pmc_traffic(f"{dom}:{cfg.scenario}:N{N}:B{B}"),
+                        traffic=pmc_traffic(f"{'lag' if (lag and dom == 'step') else dom}:{cfg.scenario}:N{N}:B{B}"),
                         algorithmic_bytes_per_launch=int(k["bytes"]), mean_launch_us=round(k["ms"] * 1e3, 3),
                         timing=f"HIP events around {L} back-to-back graph launches of the kernel",
                         other_kernel=dict(kernel=other["kernel"], achieved=round(other["gbs"], 1),
@@ -362,7 +380,9 @@ def main():
                        "agents_per_step": agents,
                        "episode_length": EL, "mean_edges_per_env": round(total_edges / B, 2),
                        "parallelism": f"env-sharded x{world} (no data-path collective)",
-                       "launch": "eager" if args.eager else "hip-graph per 100-step episode"},
+                       "launch": "eager" if args.eager else ("hip-graph per 100-step episode" + (
+                           ", lagged emission (one launch per step)" if (seg_cfg and not args.unfused)
+                           else ", step + emit launch per step"))},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }

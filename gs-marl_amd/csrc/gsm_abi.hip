@@ -23,6 +23,7 @@ struct gsm_handle {
     std::string err;
     // graph capture
     hipStream_t cap_stream = nullptr;
+    int32_t *bsum_alt = nullptr;   // second half of the per-workgroup edge-sum double buffer (lagged emission)
     struct Slot {
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
@@ -404,6 +405,14 @@ static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_
     int kern = flags & (GSM_GRAPH_STEP | GSM_GRAPH_EMIT);
     if (!kern) kern = GSM_GRAPH_STEP | GSM_GRAPH_EMIT;
     const bool each = (flags & GSM_GRAPH_TIME_EACH) != 0, ends = (flags & GSM_GRAPH_TIME_ENDS) != 0;
+    const bool lag_only = (flags & GSM_GRAPH_LAG_ONLY) != 0;
+    const bool can_lag = gsm::lag_step_kernel_fn(h->dp) != nullptr;
+    if (lag_only && (!can_lag || each || (flags & (GSM_GRAPH_STEP | GSM_GRAPH_EMIT | GSM_GRAPH_UNFUSED))))
+        return fail(h, GSM_EINVAL, "GSM_GRAPH_LAG_ONLY: segmented configs only, no other kernel/timing-each flags");
+    if (lag_only) kern = GSM_GRAPH_STEP;
+    // lagged emission: step_0, lag_step_1 .. lag_step_{T-1}, emit_{T-1}
+    const bool lag = lag_only || (can_lag && !each && kern == (GSM_GRAPH_STEP | GSM_GRAPH_EMIT) &&
+                                  !(flags & GSM_GRAPH_UNFUSED));
     if ((kern & GSM_GRAPH_STEP) && (!actions || n_actions < 1 || stride < 0))
         return fail(h, GSM_EINVAL, "bad capture arguments");
     if (n_steps < 1) return fail(h, GSM_EINVAL, "n_steps must be >= 1");
@@ -411,6 +420,10 @@ static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_
     gsm_handle::Slot &sl = h->slots[slot];
     drop_slot(sl);
     hipError_t e;
+    if (lag && !h->bsum_alt) {
+        e = hipMalloc(&h->bsum_alt, (size_t)h->sz.n_blocks * sizeof(int32_t) + 16);
+        if (e != hipSuccess) { h->bsum_alt = nullptr; return hip_fail(h, e, "hipMalloc (edge-sum buffer)"); }
+    }
     if (!h->cap_stream) {
         e = hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking);
         if (e != hipSuccess) return hip_fail(h, e, "hipStreamCreate");
@@ -449,7 +462,7 @@ static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_
         hipKernelNodeParams kp = {};
         void *args[] = {&p};
         kp.func = const_cast<void *>(fn);
-        kp.gridDim = dim3(fn == gsm::step_kernel_fn(p) ? gsm::step_grid_blocks(p) : gsm::grid_blocks(p));
+        kp.gridDim = dim3(fn == gsm::emit_kernel_fn(p) ? gsm::grid_blocks(p) : gsm::step_grid_blocks(p));
         kp.blockDim = dim3(gsm::block_threads(p));
         kp.sharedMemBytes = (unsigned)lds;
         kp.kernelParams = args;
@@ -462,6 +475,11 @@ static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_
     what = "event node";
     e = n_ev ? add_event(sl.events[0]) : hipSuccess;
     const gsm::DevParams p_bound = p;
+    // edge-sum halves: the bound buffer holds the sums of the current state
+    // before and after every graph (eager emits read it); a lagged chain
+    // alternates so that its last step writes the bound half.
+    int32_t *half[2] = {p_bound.block_edge_sum, h->bsum_alt};
+    gsm::DevParams last = p_bound;   // outputs of the previous step
     for (int t = 0; t < n_steps && e == hipSuccess; ++t) {
         at = t;
         if (per_step) {
@@ -472,17 +490,27 @@ static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_
                 return rc;
             }
         }
+        const bool lag_node = lag && (lag_only || t > 0);
+        if (lag) {
+            // lag-only: node t reads half t%2; chain: node t writes half (T-1-t)%2
+            const int w = lag_only ? (t + 1) % 2 : (n_steps - 1 - t) % 2;
+            p.block_edge_sum = half[w];
+            p.lag = gsm::DevParams::Lag{half[1 - w], last.edge_count, last.edge_ptr, last.edge_index,
+                                        last.edge_attr, last.edge_capacity};
+        }
         if (kern & GSM_GRAPH_STEP) {
             p.actions = (const char *)actions + (int64_t)(t % n_actions) * stride;
-            what = "step kernel node";
-            e = add_kernel(gsm::step_kernel_fn(p), gsm::step_kernel_lds(p));
+            what = lag_node ? "lagged step kernel node" : "step kernel node";
+            e = add_kernel(lag_node ? gsm::lag_step_kernel_fn(p) : gsm::step_kernel_fn(p), gsm::step_kernel_lds(p));
             if (e == hipSuccess && each) { what = "event node"; e = add_event(sl.events[2 * t + 1]); }
         }
-        if (e == hipSuccess && (kern & GSM_GRAPH_EMIT)) {
+        // the two-kernel chain emits every step; a lagged chain only the last
+        if (e == hipSuccess && (kern & GSM_GRAPH_EMIT) && (!lag || t == n_steps - 1)) {
             what = "emit kernel node";
             e = add_kernel(gsm::emit_kernel_fn(p), gsm::emit_kernel_lds(p));
         }
         if (e == hipSuccess && each) { what = "event node"; e = add_event(sl.events[2 * t + 2]); }
+        last = p;
     }
     if (e == hipSuccess && ends && !each) { what = "event node"; e = add_event(sl.events[1]); }
     if (e != hipSuccess) {
@@ -568,6 +596,7 @@ int gsm_destroy(gsm_handle *h) {
     if (!h) return GSM_OK;
     drop_graph(h);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
+    if (h->bsum_alt) (void)hipFree(h->bsum_alt);
     delete h;
     return GSM_OK;
 }

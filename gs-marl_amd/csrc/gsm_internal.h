@@ -56,6 +56,25 @@ struct DevParams {
     const void *actions;
     const uint8_t *env_mask;
     uint64_t *stamps;         // diagnostic builds only (GSM_STAMPS): [waves][8] s_memtime
+    // Lagged emission (segmented path, graph chains): a fused step kernel
+    // first emits the edges of the PREVIOUS step (its positions and row masks
+    // are this launch's inputs) into these outputs, using the per-workgroup
+    // edge sums the previous launch wrote to `block_sum`; this launch writes
+    // its own sums to block_edge_sum (the other half of a double buffer).
+    struct Lag {
+        const int32_t *block_sum, *edge_count;
+        int64_t *edge_ptr;
+        int32_t *edge_index;
+        float *edge_attr;
+        int64_t cap;
+    } lag;
+};
+
+// where an emission writes its edges
+struct EdgeSink {
+    int32_t *index;   // [2][cap]: sources, then destinations
+    float *attr;
+    int64_t cap;
 };
 
 // Launch the step kernel (physics / reset / observe by p.mode) and the edge
@@ -67,6 +86,10 @@ int step_grid_blocks(const DevParams &p);   // step kernel workgroups
 const void *step_kernel_fn(const DevParams &p);
 const void *emit_kernel_fn(const DevParams &p);
 const void *step_seg_kernel_fn(const DevParams &p);
+// step kernel that emits the previous step's edges first (p.lag); nullptr
+// where the path has none (tile, ragged)
+const void *lag_step_kernel_fn(const DevParams &p);
+const void *lag_step_seg_kernel_fn(const DevParams &p);
 const void *emit_seg_kernel_fn(const DevParams &p);
 const void *step_ragged_kernel_fn();
 const void *step_tile_kernel_fn();

@@ -12,6 +12,12 @@
 //   ragged     polygon / line / mixed: one wave per env, per-env shape,
 //              per-step assignment (gsm_ragged_kernels.hip).
 //
+// Inside a graph chain the segmented family can fuse the emitter of step t
+// into the step kernel of step t+1 ("lagged emission"): the
+// edges of step t are functions of the positions and row masks that step t+1
+// loads anyway, so the chain is step_0, lag_step_1, ..., lag_step_{T-1},
+// emit_{T-1}: one launch per step instead of two.
+//
 // Launches go through hipLaunchKernel with the family's kernel pointers; the
 // HIP-graph builder (gsm_abi.hip) uses the same pointers, grid and LDS sizes.
 #include "gsm_device.h"
@@ -31,13 +37,17 @@ const void *step_kernel_fn(const DevParams &p) {
     if (p.path == kPathTile) return step_tile_kernel_fn();
     return step_seg_kernel_fn(p);
 }
+const void *lag_step_kernel_fn(const DevParams &p) {
+    return p.path == kPathSeg ? lag_step_seg_kernel_fn(p) : nullptr;
+}
 const void *emit_kernel_fn(const DevParams &p) {
     if (p.path == kPathRagged) return emit_ragged_kernel_fn();
     if (p.path == kPathTile) return emit_tile_kernel_fn();
     return emit_seg_kernel_fn(p);
 }
 size_t step_kernel_lds(const DevParams &p) {
-    return p.path == kPathTile ? (size_t)p.wave_lds_step : (size_t)kWavesPerBlock * p.wave_lds_step + 16;
+    // segmented: + per-wave edge sums and (lagged emission) per-wave prefix words
+    return p.path == kPathTile ? (size_t)p.wave_lds_step : (size_t)kWavesPerBlock * p.wave_lds_step + 32;
 }
 size_t emit_kernel_lds(const DevParams &p) {
     return p.path == kPathTile ? (size_t)p.wave_lds_emit : (size_t)kWavesPerBlock * p.wave_lds_emit + 16;

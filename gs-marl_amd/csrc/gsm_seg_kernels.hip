@@ -26,7 +26,10 @@
 // (agent rows, goal rows, obstacle rows) -> lane scan -> each lane writes its
 // row (agent columns, own goal, obstacle columns); agent lanes also write the
 // goal rows. CSR offsets come from the per-workgroup sums of the step kernel:
-// no atomics, no inter-workgroup waiting, deterministic.
+// no atomics, no inter-workgroup waiting, deterministic. In a graph chain the
+// same emission runs at the top of the NEXT step kernel (kLag: the previous
+// step's positions and masks are that kernel's inputs; block_emit), so a
+// step costs one launch.
 //
 // With one env per wave (G = 1, e.g. 24 agents) the segment collectives are
 // DPP wave scans/reductions and per-env scalars are scalar loads.
@@ -238,8 +241,9 @@ __device__ __forceinline__ void store_row(float *nf, float2 v, float2 pos, float
 // its row (agent columns, own goal, obstacle columns); agent lanes also
 // write the goal rows.
 template <int kN, int kNo, int kG>
-__device__ __forceinline__ void emit_rows(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L,
-                                          const float2 *s_pos, uint64_t mask, int64_t env_off) {
+__device__ __forceinline__ void emit_rows(const Shape<kN, kNo> &s, const Lane &L, const float2 *s_pos,
+                                          uint64_t mask, int64_t env_off, const EdgeSink &out,
+                                          bool checked = true) {
     const int N = s.N, E = s.E;
     const int m = L.m;
     const int64_t eb = L.live ? L.b : 0;
@@ -253,45 +257,115 @@ __device__ __forceinline__ void emit_rows(const DevParams &p, const Shape<kN, kN
         incl = seg_scan(c, m);
         a_total = __shfl(incl, L.base + N - 1);
     }
-    int64_t o = env_off + incl - c + (m >= N ? N : 0);
+    // offsets fit in 32 bits (edge capacity < 2^31, gsm_query_sizes), so the
+    // stores take the SGPR base + 32-bit VGPR offset form
+    uint32_t o = (uint32_t)env_off + (uint32_t)(incl - c + (m >= N ? N : 0));
     if (!L.live) return;
 
     const float2 pm = s_pos[row_entity(m, N)];
-    const int64_t cap = p.edge_capacity;   // redirected outputs may be smaller than the worst case
-    int32_t *src = p.edge_index, *dst = p.edge_index + cap;
-    float *attr = p.edge_attr;
+    const uint32_t cap = (uint32_t)out.cap;   // redirected outputs may be smaller than the worst case
+    int32_t *src = out.index, *dst = out.index + cap;
+    float *attr = out.attr;
     const int32_t g0 = (int32_t)(eb * E);
     const int32_t gs = g0 + row_entity(m, N);
     const uint64_t agent_bits = N >= 64 ? ~0ull : ((1ull << N) - 1);
-    uint64_t lo = mask & agent_bits, hi = mask & ~agent_bits;
-    auto put = [&](int64_t at, int32_t a, int32_t b, float d) {
-        if (at < cap) {
-            src[at] = a;
-            dst[at] = b;
-            attr[at] = d;
+    // the same walk with and without the capacity test (an env that fits
+    // entirely, the normal case, stores unchecked)
+    auto walk = [&](auto chk) {
+        constexpr bool kChecked = decltype(chk)::value;
+        auto put = [&](uint32_t at, int32_t a, int32_t b, float d) {
+            if (!kChecked || at < cap) {
+                src[at] = a;
+                dst[at] = b;
+                attr[at] = d;
+            }
+        };
+        uint64_t lo = mask & agent_bits, hi = mask & ~agent_bits;
+        while (lo) {
+            const int j = __builtin_ctzll(lo);
+            lo &= lo - 1;
+            const float2 q = s_pos[j];
+            const float dx = pm.x - q.x, dy = pm.y - q.y;
+            put(o++, gs, g0 + j, __builtin_amdgcn_sqrtf(dx * dx + dy * dy));
+        }
+        if (L.agent) {
+            const float2 g = s_pos[N + m];
+            const float dx = pm.x - g.x, dy = pm.y - g.y;
+            const float d = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+            put(o++, gs, g0 + N + m, d);                  // agent m -> its goal
+            put((uint32_t)env_off + (uint32_t)(a_total + m), g0 + N + m, gs, d);  // goal row: goal m -> agent m
+        }
+        while (hi) {
+            const int j = __builtin_ctzll(hi);
+            hi &= hi - 1;
+            const float2 q = s_pos[N + j];
+            const float dx = pm.x - q.x, dy = pm.y - q.y;
+            put(o++, gs, g0 + N + j, __builtin_amdgcn_sqrtf(dx * dx + dy * dy));
         }
     };
-    while (lo) {
-        const int j = __builtin_ctzll(lo);
-        lo &= lo - 1;
-        const float2 q = s_pos[j];
-        const float dx = pm.x - q.x, dy = pm.y - q.y;
-        put(o++, gs, g0 + j, __builtin_amdgcn_sqrtf(dx * dx + dy * dy));
+    if (checked) walk(std::true_type{});
+    else walk(std::false_type{});
+}
+
+// CSR offsets of a workgroup's envs: its edge counts (lane k < envs of the
+// block: env first+k) and the sum of the preceding workgroups' edge sums
+// (int4 loads spread over the workgroup's threads). Loads only; the sums are
+// reduced in block_emit after the caller's other loads are in flight.
+struct BlockPrefix {
+    int cnt_k, acc;
+};
+__device__ __forceinline__ BlockPrefix block_prefix_loads(const int32_t *block_sum, const int32_t *edge_count,
+                                                          int B, int G) {
+    BlockPrefix r{0, 0};
+    const int lane = threadIdx.x & 63;
+    const int first = blockIdx.x * kWavesPerBlock * G;
+    const int nblk = min(kWavesPerBlock * G, B - first);
+    if (lane < nblk) r.cnt_k = edge_count[first + lane];
+#ifdef GSM_ABL_NO_PREFIX   // timing-only ablation build (wrong offsets)
+    if (false)
+#endif
+    {
+        const int nb = (int)blockIdx.x;
+        const int nb4 = nb & ~3;
+        const int4 *bs4 = (const int4 *)block_sum;
+        for (int k = threadIdx.x; 4 * k < nb4; k += kBlock) {
+            const int4 q = bs4[k];
+            r.acc += q.x + q.y + q.z + q.w;
+        }
+        if ((int)threadIdx.x < nb - nb4) r.acc += block_sum[nb4 + threadIdx.x];
     }
-    if (L.agent) {
-        const float2 g = s_pos[N + m];
-        const float dx = pm.x - g.x, dy = pm.y - g.y;
-        const float d = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-        put(o++, gs, g0 + N + m, d);                  // agent m -> its goal
-        put(env_off + a_total + m, g0 + N + m, gs, d);  // goal row: goal m -> agent m
+    return r;
+}
+
+// Workgroup-wide (every wave of the block must call it: one barrier): the
+// env's global offset from the loaded prefix, its edge_ptr entry, then its
+// edges. s_red: kWavesPerBlock ints of LDS.
+template <int kN, int kNo, int kG>
+__device__ __forceinline__ void block_emit(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L,
+                                           const float2 *s_pos, uint64_t mask, BlockPrefix pre, int *s_red,
+                                           int64_t *edge_ptr, const EdgeSink &out) {
+    const int first = blockIdx.x * kWavesPerBlock * s.G;
+    const int acc = wave_total(pre.acc);
+    if (L.lane == 0) s_red[L.wave] = acc;
+    const int incl_k = wave_scan(pre.cnt_k);     // envs of this block in order
+    __syncthreads();
+    int64_t base = 0;
+    for (int q = 0; q < kWavesPerBlock; ++q) base += s_red[q];
+    int my_cnt, before;
+    if constexpr (kG == 1) {
+        my_cnt = __builtin_amdgcn_readlane(pre.cnt_k, L.wave);
+        before = __builtin_amdgcn_readlane(incl_k, L.wave) - my_cnt;
+    } else {
+        const int kk = L.live ? L.b - first : 0;
+        my_cnt = __shfl(pre.cnt_k, kk);
+        before = __shfl(incl_k, kk) - my_cnt;
     }
-    while (hi) {
-        const int j = __builtin_ctzll(hi);
-        hi &= hi - 1;
-        const float2 q = s_pos[N + j];
-        const float dx = pm.x - q.x, dy = pm.y - q.y;
-        put(o++, gs, g0 + N + j, __builtin_amdgcn_sqrtf(dx * dx + dy * dy));
+    const int64_t env_off = base + before;
+    if (L.live && L.m == 0) {
+        edge_ptr[L.b] = env_off;
+        if (L.b == p.B - 1) edge_ptr[p.B] = env_off + my_cnt;
     }
+    emit_rows<kN, kNo, kG>(s, L, s_pos, mask, env_off, out, env_off + my_cnt > out.cap);
 }
 
 // ---------------------------------------------------------------------------
@@ -312,7 +386,7 @@ struct SegIn {
     float2 acc;
 };
 
-template <int kN, int kNo, int kFmt>
+template <int kN, int kNo, int kFmt, bool kLag>
 __device__ __forceinline__ SegIn seg_load(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L) {
     SegIn in;
     in.x0 = in.x1 = in.v = in.u = make_float2(0.0f, 0.0f);
@@ -336,16 +410,19 @@ __device__ __forceinline__ SegIn seg_load(const DevParams &p, const Shape<kN, kN
                 in.cand_prev = (p.contact_mask + eb * N)[um];
             }
         }
-        if (L.live && L.m >= N && p.mode == kModeStep) in.oo = (p.row_mask + eb * M)[um];
+        // obstacle rows: cached obstacle-obstacle bits; lagged emission: every
+        // row (the previous step's masks)
+        if (L.live && (kLag || L.m >= N) && p.mode == kModeStep) in.oo = (p.row_mask + eb * M)[um];
     }
     return in;
 }
 
 // One env (G = 1) or one wave's G envs: everything after the loads. Returns
 // the wave's edge count (the sum over its envs).
-template <int kN, int kNo, int kFmt>
+template <int kN, int kNo, int kFmt, bool kLag>
 __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L,
-                                       unsigned char *wave_lds, const SegIn &in, int64_t wid) {
+                                       unsigned char *wave_lds, const SegIn &in, int64_t wid,
+                                       BlockPrefix lag_pre, int *s_lag) {
     constexpr int kG = envs_per_wave<kN, kNo>();
     const int N = s.N, E = s.E, M = s.M, G = s.G;
     const int segc = L.seg < G ? L.seg : G - 1;             // clamp idle lanes' addresses
@@ -385,10 +462,15 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
                 cand_prev = p.contact_mask[eb * N + m];
             }
         }
-        if (obst && p.mode == kModeStep) oo = p.row_mask[eb * M + m];
+        if ((kLag ? L.live : obst) && p.mode == kModeStep) oo = p.row_mask[eb * M + m];
     }
     bool reset = L.live && p.mode == kModeReset && (p.env_mask == nullptr || p.env_mask[L.b] != 0);
     wave_sync();
+    if constexpr (kLag) {
+        // the previous step's edges: its positions (staged above) and row masks
+        block_emit<kN, kNo, kG>(p, s, L, s_pos, oo, lag_pre, s_lag, p.lag.edge_ptr,
+                                EdgeSink{p.lag.edge_index, p.lag.edge_attr, p.lag.cap});
+    }
 
     // scenario.reset_world (Philox layout, App. A S14) for the lanes' envs
     auto relayout = [&]() {
@@ -542,7 +624,8 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     }
 
 #ifdef GSM_ABL_FUSED_PADDED   // timing-only: emit here at a fixed per-env stride
-    emit_rows<kN, kNo, kG>(p, s, L, s_pos, row, (int64_t)(L.live ? L.b : 0) * (p.edge_capacity / p.B));
+    emit_rows<kN, kNo, kG>(s, L, s_pos, row, (int64_t)(L.live ? L.b : 0) * (p.edge_capacity / p.B),
+                           EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity});
 #endif
     // edge count (radius rows + goal edges both ways)
     const int edges = __popcll(row) + ((L.live && m == 0) ? 2 * N : 0);
@@ -570,7 +653,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     return wave_edges;
 }
 
-template <int kN, int kNo, int kFmt>
+template <int kN, int kNo, int kFmt, bool kLag>
 __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Shape<kN, kNo> s(p);
@@ -580,11 +663,14 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
     unsigned char *wave_lds = smem + wave * p.wave_lds_step;
     const int64_t wid = (int64_t)blockIdx.x * kWavesPerBlock + wave;
     int *s_bc = (int *)(smem + kWavesPerBlock * p.wave_lds_step);
+    int *s_lag = s_bc + kWavesPerBlock;
     GSM_RSTAMP(p, wid, 8);
     {
         SegIn in{};
-        if constexpr (kG == 1) in = seg_load<kN, kNo, kFmt>(p, s, L);
-        const int edges = seg_env<kN, kNo, kFmt>(p, s, L, wave_lds, in, wid);
+        if constexpr (kG == 1) in = seg_load<kN, kNo, kFmt, kLag>(p, s, L);
+        BlockPrefix lag_pre{0, 0};
+        if constexpr (kLag) lag_pre = block_prefix_loads(p.lag.block_sum, p.lag.edge_count, p.B, s.G);
+        const int edges = seg_env<kN, kNo, kFmt, kLag>(p, s, L, wave_lds, in, wid, lag_pre, s_lag);
         if (L.lane == 0) s_bc[wave] = edges;
         __syncthreads();
         if (threadIdx.x == 0) {
@@ -614,68 +700,32 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
     GSM_RSTAMP(p, wid, 8);
     GSM_STAMP(p, wid, 0);
 
-    // inputs independent of the prefix first
+    // every global load first (positions, row masks, the block's edge counts,
+    // the preceding blocks' sums), then the first wait
+    const BlockPrefix pre = block_prefix_loads(p.block_edge_sum, p.edge_count, p.B, G);
     uint64_t mask = 0;
+    float2 x0 = make_float2(0.0f, 0.0f), x1 = x0;
     if constexpr (kG == 1) {
         if (L.b < p.B) {
             const float2 *src = p.pos + (int64_t)L.b * E;
-            if (L.lane < E) s_pos[L.lane] = src[L.lane];
-            if (L.lane + kWave < E) s_pos[L.lane + kWave] = src[L.lane + kWave];
+            if (L.lane < E) x0 = src[L.lane];
+            if (L.lane + kWave < E) x1 = src[L.lane + kWave];
             if (L.live) mask = p.row_mask[eb * M + m];
         }
     } else if (L.live) {
-        for (int e = m; e < E; e += M) s_pos[e] = p.pos[eb * E + e];
         mask = p.row_mask[eb * M + m];
     }
-    // global offset of this block: prefix of the step kernel's block sums
-    int acc = 0;
-#ifdef GSM_ABL_NO_PREFIX   // timing-only ablation build (wrong offsets)
-    if (false)
-#endif
-    {
-        const int nb = (int)blockIdx.x;
-        const int nb4 = nb & ~3;
-        const int4 *bs4 = (const int4 *)p.block_edge_sum;
-        for (int k = threadIdx.x; 4 * k < nb4; k += kBlock) {
-            const int4 q = bs4[k];
-            acc += q.x + q.y + q.z + q.w;
-        }
-        if ((int)threadIdx.x < nb - nb4) acc += p.block_edge_sum[nb4 + threadIdx.x];
-    }
-    acc = wave_total(acc);
-    GSM_STAMP(p, wid, 1);
-    if (L.lane == 0) s_red[wave] = acc;
-    // envs of this block in order before this lane's env
-    int64_t env_off;
-    int my_cnt;
     if constexpr (kG == 1) {
-        const int first = blockIdx.x * kWavesPerBlock;
-        int before = 0;
-        for (int q = 0; q < wave; ++q) before += p.edge_count[first + q];
-        my_cnt = L.b < p.B ? p.edge_count[L.b] : 0;
-        __syncthreads();
-        int64_t base = 0;
-        for (int q = 0; q < kWavesPerBlock; ++q) base += s_red[q];
-        env_off = base + before;
-    } else {
-        const int first = blockIdx.x * kWavesPerBlock * G;
-        const int nblk = min(kWavesPerBlock * G, p.B - first);
-        const int cnt_k = L.lane < nblk ? p.edge_count[first + L.lane] : 0;
-        const int incl_k = wave_scan(cnt_k);
-        __syncthreads();
-        int64_t base = 0;
-        for (int q = 0; q < kWavesPerBlock; ++q) base += s_red[q];
-        const int kk = L.live ? L.b - first : 0;
-        my_cnt = __shfl(cnt_k, kk);
-        env_off = base + __shfl(incl_k, kk) - my_cnt;
+        if (L.b < p.B) {
+            if (L.lane < E) s_pos[L.lane] = x0;
+            if (L.lane + kWave < E) s_pos[L.lane + kWave] = x1;
+        }
+    } else if (L.live) {
+        for (int e = m; e < E; e += M) s_pos[e] = p.pos[eb * E + e];
     }
-    if (L.live && m == 0) {
-        p.edge_ptr[L.b] = env_off;
-        if (L.b == p.B - 1) p.edge_ptr[p.B] = env_off + my_cnt;
-    }
-    GSM_STAMP(p, wid, 2);
-
-    emit_rows<kN, kNo, kG>(p, s, L, s_pos, mask, env_off);
+    GSM_STAMP(p, wid, 1);
+    block_emit<kN, kNo, kG>(p, s, L, s_pos, mask, pre, s_red, p.edge_ptr,
+                            EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity});
     GSM_STAMP(p, wid, 4);
     GSM_RSTAMP(p, wid, 9);
 }
@@ -685,19 +735,22 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
 // runtime-shape instantiation.
 #define GSM_SEG_SHAPES(X) X(3, 3) X(24, 24)
 
-const void *step_seg_kernel_fn(const DevParams &p) {
+template <bool LAG>
+static const void *pick_step_seg(const DevParams &p) {
 #define GSM_PICK(n, no)                                                                       \
     if (p.N == n && p.No == no) {                                                             \
         switch (p.action_fmt) {                                                               \
-            case 0: return reinterpret_cast<const void *>(&gsm_step_seg_kernel<n, no, 0>);    \
-            case 1: return reinterpret_cast<const void *>(&gsm_step_seg_kernel<n, no, 1>);    \
-            default: return reinterpret_cast<const void *>(&gsm_step_seg_kernel<n, no, 2>);   \
+            case 0: return reinterpret_cast<const void *>(&gsm_step_seg_kernel<n, no, 0, LAG>); \
+            case 1: return reinterpret_cast<const void *>(&gsm_step_seg_kernel<n, no, 1, LAG>); \
+            default: return reinterpret_cast<const void *>(&gsm_step_seg_kernel<n, no, 2, LAG>); \
         }                                                                                     \
     }
     GSM_SEG_SHAPES(GSM_PICK)
 #undef GSM_PICK
-    return reinterpret_cast<const void *>(&gsm_step_seg_kernel<0, 0, -1>);
+    return reinterpret_cast<const void *>(&gsm_step_seg_kernel<0, 0, -1, LAG>);
 }
+const void *step_seg_kernel_fn(const DevParams &p) { return pick_step_seg<false>(p); }
+const void *lag_step_seg_kernel_fn(const DevParams &p) { return pick_step_seg<true>(p); }
 
 const void *emit_seg_kernel_fn(const DevParams &p) {
 #define GSM_PICK(n, no) \

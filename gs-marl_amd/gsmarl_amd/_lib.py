@@ -16,6 +16,7 @@ ABI_VERSION = 3
 GSM_OK, GSM_EINVAL, GSM_EHIP, GSM_ESTATE = 0, -1, -2, -3
 GRAPH_SLOTS = 4
 GRAPH_STEP, GRAPH_EMIT, GRAPH_TIME_EACH, GRAPH_TIME_ENDS = 1, 2, 4, 8
+GRAPH_UNFUSED, GRAPH_LAG_ONLY = 16, 32
 ACT_ONEHOT, ACT_INDEX, ACT_CONT = 0, 1, 2
 
 

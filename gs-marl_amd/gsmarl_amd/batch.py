@@ -214,10 +214,15 @@ class GpuBatchEnv:
                 slot: int = 0, kernels: str = "both", time_ends: bool = False) -> None:
         """Build HIP graph ``slot`` of ``n_steps`` steps; the j-th step uses
         ``actions_seq[j % len(actions_seq)]`` (a [T, B, N(,k)] device tensor).
-        kernels: "both", "step" or "emit" (re-emits the current edges).
-        timing: event nodes around every kernel; time_ends: only around the
-        whole graph (per-kernel means over back-to-back launches)."""
-        flags = {"both": 0, "step": _lib.GRAPH_STEP, "emit": _lib.GRAPH_EMIT}[kernels]
+        kernels: "both" (segmented configs: lagged emission, one launch per
+        step), "unfused" (step + emit kernel per step), "step", "emit"
+        (re-emits the current edges) or "lag" (lagged step kernels only; the
+        last step's edges are left unemitted — a timing tool).
+        timing: event nodes around every kernel (implies "unfused");
+        time_ends: only around the whole graph (per-kernel means over
+        back-to-back launches)."""
+        flags = {"both": 0, "unfused": _lib.GRAPH_UNFUSED, "step": _lib.GRAPH_STEP, "emit": _lib.GRAPH_EMIT,
+                 "lag": _lib.GRAPH_LAG_ONLY}[kernels]
         if timing:
             flags |= _lib.GRAPH_TIME_EACH
         if time_ends:

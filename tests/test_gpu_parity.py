@@ -259,6 +259,70 @@ def test_graph_replay_equals_eager_and_deterministic():
     assert torch.equal(eager["pos"], env.t["pos"])
 
 
+@pytest.mark.parametrize("N,B,T", [(24, 256, 40), (24, 257, 7), (3, 4000, 1), (3, 123, 2), (5, 37, 9), (7, 64, 6)])
+def test_lagged_chain_equals_eager(N, B, T):
+    """Segmented graphs emit step j's edges from step j+1's kernel (lagged
+    emission): the chain must leave every state and output buffer exactly as
+    eager steps and as the two-kernel chain do, for odd and even chain
+    lengths, partial workgroups and auto-resets (episode length 5)."""
+    env, ocfg = _env(n_agents=N, n_envs=B, episode_length=5)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    keys = ("pos", "vel", "step_count", "episode", "node_feat", "reward", "cost", "done", "edge_count",
+            "edge_ptr", "ep_acc", "ep_last", "row_mask", "contact_mask")
+    env.reset(seed=6)
+    for t in range(T):
+        env.step(acts[t], sync_edges=False)
+    torch.cuda.synchronize()
+    eager = {k: v.clone() for k, v in env.t.items()}
+    n = int(eager["edge_ptr"][-1])
+    for kernels, slot in (("both", 0), ("unfused", 1)):
+        env.reset(seed=6)
+        env.capture(acts, T, slot=slot, kernels=kernels)
+        env.replay(slot)
+        torch.cuda.synchronize()
+        for k in keys:
+            assert torch.equal(eager[k], env.t[k]), (kernels, k)
+        assert torch.equal(eager["edge_index"][:, :n], env.t["edge_index"][:, :n]), kernels
+        assert torch.equal(eager["edge_attr"][:n], env.t["edge_attr"][:n]), kernels
+        # the bound edge-sum buffer holds the last step's sums: an emit-only
+        # graph right after the chain re-emits the same edges
+        env.t["edge_index"].zero_()
+        env.capture(None, 1, slot=3, kernels="emit")
+        env.replay(3)
+        torch.cuda.synchronize()
+        assert torch.equal(eager["edge_ptr"], env.t["edge_ptr"]), kernels
+        assert torch.equal(eager["edge_index"][:, :n], env.t["edge_index"][:, :n]), kernels
+    env.close()
+
+
+def test_lag_only_graph():
+    """The lagged-kernel timing graph: physics like eager steps; its last
+    emission is that of the step before the last."""
+    env, ocfg = _env(n_agents=24, n_envs=300, episode_length=1000)
+    T = 6
+    acts = torch.randint(0, 5, (T, 300, 24), dtype=torch.int32, device=DEV)
+    env.reset(seed=9)
+    for t in range(T - 1):
+        env.step(acts[t], sync_edges=False)
+    torch.cuda.synchronize()
+    before_last = {k: env.t[k].clone() for k in ("edge_ptr", "edge_index", "edge_attr")}
+    env.step(acts[T - 1], sync_edges=False)
+    eager = {k: v.clone() for k, v in env.t.items()}
+    env.reset(seed=9)
+    env.capture(acts, T, slot=2, kernels="lag", time_ends=True)
+    env.replay(2)
+    torch.cuda.synchronize()
+    for k in ("pos", "vel", "step_count", "node_feat", "reward", "cost", "edge_count"):
+        assert torch.equal(eager[k], env.t[k]), k
+    n = int(before_last["edge_ptr"][-1])
+    assert torch.equal(before_last["edge_ptr"], env.t["edge_ptr"])
+    assert torch.equal(before_last["edge_index"][:, :n], env.t["edge_index"][:, :n])
+    assert torch.equal(before_last["edge_attr"][:n], env.t["edge_attr"][:n])
+    s_ms, e_ms, tot = env.graph_kernel_ms(2)
+    assert s_ms > 0 and e_ms == 0
+    env.close()
+
+
 def test_kernel_only_graphs():
     """Roofline timing graphs: a step-only graph advances the physics exactly
     like eager steps; an emit-only graph re-emits the same edges (idempotent)."""

@@ -54,11 +54,13 @@ def test_eager_rollout_matches_plain_env(kw):
     ref.close()
 
 
-def test_graph_rollout_matches_eager():
+@pytest.mark.parametrize("N,B,T", [(24, 128, 9), (24, 130, 8), (3, 100, 1), (3, 100, 2), (5, 37, 7), (80, 6, 5)])
+def test_graph_rollout_matches_eager(N, B, T):
+    """The graph chain (segmented configs: lagged emission, slot j's edges
+    written by step j+1's kernel) equals eager step_into slot by slot."""
     from gsmarl_amd import GraphRolloutBuffer
-    env, ref = _pair(n_agents=24, n_envs=128, seed=2, episode_length=6)
-    T = 9
-    acts = torch.randint(0, 5, (T, 128, 24), dtype=torch.int32, device=DEV)
+    env, ref = _pair(n_agents=N, n_envs=B, seed=2, episode_length=6)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
     gb = GraphRolloutBuffer(env, episode_length=T)
     eb = GraphRolloutBuffer(ref, episode_length=T)
     gb.reset(seed=2)
@@ -71,8 +73,9 @@ def test_graph_rollout_matches_eager():
     for k in ("node_feat", "reward", "cost", "done", "edge_ptr", "edge_count", "actions"):
         assert torch.equal(getattr(gb, k), getattr(eb, k)), k
     for t in range(T + 1):
-        n = int(gb.edge_ptr[t, 128])
+        n = int(gb.edge_ptr[t, B])
         assert torch.equal(gb.edge_index[t][:, :n], eb.edge_index[t][:, :n])
+        assert torch.equal(gb.edge_attr[t][:n], eb.edge_attr[t][:n])
     env.close()
     ref.close()
 

@@ -30,6 +30,9 @@ def med(kernels, idx):
 
 s = med("step", 0)
 e = med("emit", 1)
-tot = med("both", 2) / 100
-print(json.dumps({"lib": os.environ.get("GSM_LIB_PATH", "default"), "N": N, "B": B, "scenario": scn,
-                  "step_ms": s, "emit_ms": e, "step_total_ms": tot}))
+out = {"lib": os.environ.get("GSM_LIB_PATH", "default"), "N": N, "B": B, "scenario": scn,
+       "step_ms": s, "emit_ms": e, "step_total_ms_unfused": med("unfused", 2) / 100}
+if not env.cfg.ragged and env.sizes.n_colliders <= 64:   # segmented: lagged emission
+    out["lag_step_ms"] = med("lag", 0)
+out["step_total_ms"] = med("both", 2) / 100
+print(json.dumps(out))
