@@ -257,15 +257,21 @@ __device__ __forceinline__ void emit_rows(const Shape<kN, kNo> &s, const Lane &L
         incl = seg_scan(c, m);
         a_total = __shfl(incl, L.base + N - 1);
     }
-    // offsets fit in 32 bits (edge capacity < 2^31, gsm_query_sizes), so the
-    // stores take the SGPR base + 32-bit VGPR offset form
-    uint32_t o = (uint32_t)env_off + (uint32_t)(incl - c + (m >= N ? N : 0));
-    if (!L.live) return;
+    // Stores are addressed from a wave-uniform base (the offset of the wave's
+    // first env: envs are in order) plus a 32-bit byte offset, the SGPR-base
+    // + VGPR-offset store form; edge offsets fit in 32 bits (edge capacity
+    // < 2^31, gsm_query_sizes).
+    const uint32_t wb_lo = __builtin_amdgcn_readfirstlane((uint32_t)env_off);
+    const uint32_t wb_hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)env_off >> 32));
+    const int64_t wbase = (int64_t)(((uint64_t)wb_hi << 32) | wb_lo);
+    uint32_t o = (uint32_t)(env_off - wbase) + (uint32_t)(incl - c + (m >= N ? N : 0));
+    const uint32_t goal_at = (uint32_t)(env_off - wbase) + (uint32_t)(a_total + m);
+    if (!L.live || wbase >= out.cap) return;
 
     const float2 pm = s_pos[row_entity(m, N)];
-    const uint32_t cap = (uint32_t)out.cap;   // redirected outputs may be smaller than the worst case
-    int32_t *src = out.index, *dst = out.index + cap;
-    float *attr = out.attr;
+    const uint32_t cap = (uint32_t)(out.cap - wbase);   // redirected outputs may be smaller than the worst case
+    char *src = (char *)(out.index + wbase), *dst = (char *)(out.index + out.cap + wbase);
+    char *attr = (char *)(out.attr + wbase);
     const int32_t g0 = (int32_t)(eb * E);
     const int32_t gs = g0 + row_entity(m, N);
     const uint64_t agent_bits = N >= 64 ? ~0ull : ((1ull << N) - 1);
@@ -275,32 +281,49 @@ __device__ __forceinline__ void emit_rows(const Shape<kN, kNo> &s, const Lane &L
         constexpr bool kChecked = decltype(chk)::value;
         auto put = [&](uint32_t at, int32_t a, int32_t b, float d) {
             if (!kChecked || at < cap) {
-                src[at] = a;
-                dst[at] = b;
-                attr[at] = d;
+                const uint32_t byte = at << 2;
+                *(int32_t *)(src + byte) = a;
+                *(int32_t *)(dst + byte) = b;
+                *(float *)(attr + byte) = d;
             }
         };
-        uint64_t lo = mask & agent_bits, hi = mask & ~agent_bits;
-        while (lo) {
-            const int j = __builtin_ctzll(lo);
-            lo &= lo - 1;
+        auto edge_to = [&](int j, int32_t col) {     // lane's row -> entity j (staged position)
             const float2 q = s_pos[j];
             const float dx = pm.x - q.x, dy = pm.y - q.y;
-            put(o++, gs, g0 + j, __builtin_amdgcn_sqrtf(dx * dx + dy * dy));
+            put(o++, gs, col, __builtin_amdgcn_sqrtf(dx * dx + dy * dy));
+        };
+        if constexpr (kN > 0 && kN <= 32 && kNo <= 32) {
+            // compile-time shape with both halves in 32 bits
+            uint32_t lo = (uint32_t)(mask & agent_bits), hi = (uint32_t)(mask >> kN);
+            while (lo) {
+                const int j = __builtin_ctz(lo);
+                lo &= lo - 1;
+                edge_to(j, g0 + j);
+            }
+            if (L.agent) edge_to(N + m, g0 + N + m);       // agent m -> its goal
+            while (hi) {
+                const int j = __builtin_ctz(hi);
+                hi &= hi - 1;
+                edge_to(2 * N + j, g0 + 2 * N + j);
+            }
+        } else {
+            uint64_t lo = mask & agent_bits, hi = mask & ~agent_bits;
+            while (lo) {
+                const int j = __builtin_ctzll(lo);
+                lo &= lo - 1;
+                edge_to(j, g0 + j);
+            }
+            if (L.agent) edge_to(N + m, g0 + N + m);       // agent m -> its goal
+            while (hi) {
+                const int j = __builtin_ctzll(hi);
+                hi &= hi - 1;
+                edge_to(N + j, g0 + N + j);
+            }
         }
-        if (L.agent) {
+        if (L.agent) {                                      // goal row: goal m -> agent m
             const float2 g = s_pos[N + m];
             const float dx = pm.x - g.x, dy = pm.y - g.y;
-            const float d = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
-            put(o++, gs, g0 + N + m, d);                  // agent m -> its goal
-            put((uint32_t)env_off + (uint32_t)(a_total + m), g0 + N + m, gs, d);  // goal row: goal m -> agent m
-        }
-        while (hi) {
-            const int j = __builtin_ctzll(hi);
-            hi &= hi - 1;
-            const float2 q = s_pos[N + j];
-            const float dx = pm.x - q.x, dy = pm.y - q.y;
-            put(o++, gs, g0 + N + j, __builtin_amdgcn_sqrtf(dx * dx + dy * dy));
+            put(goal_at, g0 + N + m, gs, __builtin_amdgcn_sqrtf(dx * dx + dy * dy));
         }
     };
     if (checked) walk(std::true_type{});
@@ -365,6 +388,9 @@ __device__ __forceinline__ void block_emit(const DevParams &p, const Shape<kN, k
         edge_ptr[L.b] = env_off;
         if (L.b == p.B - 1) edge_ptr[p.B] = env_off + my_cnt;
     }
+#ifdef GSM_ABL_NO_ROWS   // timing-only ablation (no edges written)
+    if (my_cnt < 0)
+#endif
     emit_rows<kN, kNo, kG>(s, L, s_pos, mask, env_off, out, env_off + my_cnt > out.cap);
 }
 

@@ -8,7 +8,9 @@ OUT="$GRAFT_REPO_ROOT/gpurun_out/${TAG}"
 mkdir -p "$OUT"
 cd /tmp
 timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
-BENCH="$GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-kernel-timing --eager --steps 100 --warmup 10 $*"
+# PMC_GRAPH=1: graph replay (lagged-emission step kernels) instead of eager launches
+LAUNCH=--eager; [ -n "$PMC_GRAPH" ] && LAUNCH=
+BENCH="$GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-kernel-timing $LAUNCH --steps 100 --warmup 10 $*"
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE" \

@@ -16,7 +16,10 @@ for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), re
             name = row.get("Kernel_Name", "")
             if "gsm" not in name:
                 continue
-            short = "step" if "step" in name else ("emit" if "emit" in name else name[:40])
+            if "step" in name:   # the lagged-emission step kernel: template argument kLag = true
+                short = "lag" if ", true>" in name else "step"
+            else:
+                short = "emit" if "emit" in name else name[:40]
             acc[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
 out = {}
 for k, d in acc.items():

@@ -3,8 +3,9 @@ bench.py reads for roofline.traffic: HBM bytes per launch of each kernel =
 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes; the x2 is the gfx950 FETCH_SIZE
 correction of MI355X_MICROARCH.md section HBM/rocprofv3).
 
-Usage: python tools/pmc_traffic.py OUT_JSON KEY_PREFIX=SUMMARY_DIR ...
+Usage: python tools/pmc_traffic.py OUT_JSON [KINDS@]KEY_PREFIX=SUMMARY_DIR ...
   e.g. h:navigation:N24:B8192=gpurun_out/pmc_h  (keys: step:navigation:N24:B8192, emit:...)
+       lag@h:navigation:N24:B8192=gpurun_out/pmc_h_lag  (only the lagged step kernel)
 """
 import json
 import os
@@ -14,9 +15,15 @@ out_path = sys.argv[1]
 res = json.load(open(out_path)) if os.path.exists(out_path) else {}
 for spec in sys.argv[2:]:
     key, d = spec.split("=", 1)
+    kinds = None
+    if "@" in key:
+        k0, key = key.split("@", 1)
+        kinds = set(k0.split("+"))
     txt = open(os.path.join(d, "summary.txt")).read()
     summ = json.loads(txt[txt.index("{"):])
     for kern, v in summ.items():
+        if kinds is not None and kern not in kinds:
+            continue
         c = v["counters"]
         if "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
             continue
