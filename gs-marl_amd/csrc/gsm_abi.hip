@@ -585,6 +585,30 @@ int gsm_attn_aggregate(const float *q, const float *k, const float *v, const flo
     return GSM_OK;
 }
 
+int gsm_render(const float *node_feat, int64_t n_envs, int32_t n_entities, const int64_t *edge_ptr,
+               const int32_t *edge_index, int64_t edge_capacity, const int32_t *env_ids, int32_t n_frames,
+               float half_width, float agent_size, float target_size, float obstacle_size, int32_t width,
+               int32_t height, int32_t flags, uint8_t *rgba, void *stream) {
+    if (n_frames < 0 || n_frames > 65535) return fail(nullptr, GSM_EINVAL, "n_frames must be in [0, 65535]");
+    if (width < 1 || height < 1 || width > 8192 || height > 8192)
+        return fail(nullptr, GSM_EINVAL, "width and height must be in [1, 8192]");
+    if (n_entities < 1 || n_entities > 4096) return fail(nullptr, GSM_EINVAL, "n_entities must be in [1, 4096]");
+    if (n_envs < 1) return fail(nullptr, GSM_EINVAL, "n_envs must be >= 1");
+    if (!(agent_size >= 0.0f && target_size >= 0.0f && obstacle_size >= 0.0f))
+        return fail(nullptr, GSM_EINVAL, "sizes must be >= 0");
+    if (n_frames == 0) return GSM_OK;
+    const bool edges = (flags & GSM_RENDER_EDGES) != 0;
+    if (!node_feat || !env_ids || !rgba || (edges && (!edge_ptr || !edge_index || edge_capacity < 1)))
+        return fail(nullptr, GSM_EINVAL, "a required pointer is NULL");
+    if ((uintptr_t)rgba & 3) return fail(nullptr, GSM_EINVAL, "rgba must be 4-byte aligned");
+    const hipError_t e = gsm::launch_render(node_feat, n_envs, n_entities, edge_ptr, edge_index, edge_capacity,
+                                            env_ids, n_frames, half_width, agent_size, target_size,
+                                            obstacle_size, width, height, edges ? 1 : 0, rgba,
+                                            as_stream(stream));
+    if (e != hipSuccess) return hip_fail(nullptr, e, "gsm_render launch");
+    return GSM_OK;
+}
+
 int gsm_debug_set_stamps(gsm_handle *h, void *stamps) {
     if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
     h->dp.stamps = (uint64_t *)stamps;

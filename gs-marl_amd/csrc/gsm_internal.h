@@ -107,5 +107,9 @@ hipError_t launch_attn_aggregate(const float *q, const float *k, const float *v,
                                  const float *w_e, const int64_t *row_ptr, const int32_t *col,
                                  const float *skip, int64_t n_nodes, int HC, int C, float scale, float *out,
                                  hipStream_t s);
+hipError_t launch_render(const float *node_feat, int64_t n_envs, int32_t n_entities, const int64_t *edge_ptr,
+                         const int32_t *edge_index, int64_t edge_capacity, const int32_t *env_ids,
+                         int32_t n_frames, float half_width, float r_agent, float r_target, float r_obst,
+                         int32_t width, int32_t height, int32_t draw_edges, uint8_t *rgba_out, hipStream_t s);
 
 }  // namespace gsm

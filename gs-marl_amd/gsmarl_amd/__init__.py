@@ -7,10 +7,11 @@ from .make_env import make_env
 from .vec_env import GpuGraphVecEnv, make_eval_env, make_train_env
 from .rollout import GraphRolloutBuffer
 from . import gnn
+from . import render
 from . import distributed
 
 __version__ = "0.1.0"
 __all__ = ["EnvConfig", "GpuBatchEnv", "MultiAgentEnv", "MultiAgentConstrainEnv",
            "MultiAgentGraphConstrainEnv", "make_env", "GpuGraphVecEnv", "make_train_env", "make_eval_env",
-           "GraphRolloutBuffer", "gnn",
+           "GraphRolloutBuffer", "gnn", "render",
            "distributed"]

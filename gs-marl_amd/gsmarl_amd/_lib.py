@@ -11,12 +11,13 @@ import os
 from pathlib import Path
 
 LIB_PATH = Path(os.environ.get("GSM_LIB_PATH") or Path(__file__).resolve().parent / "lib" / "libgsm.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 GSM_OK, GSM_EINVAL, GSM_EHIP, GSM_ESTATE = 0, -1, -2, -3
 GRAPH_SLOTS = 4
 GRAPH_STEP, GRAPH_EMIT, GRAPH_TIME_EACH, GRAPH_TIME_ENDS = 1, 2, 4, 8
 GRAPH_UNFUSED, GRAPH_LAG_ONLY = 16, 32
+RENDER_EDGES = 1
 ACT_ONEHOT, ACT_INDEX, ACT_CONT = 0, 1, 2
 
 
@@ -81,6 +82,8 @@ SIGNATURES = {
                                       C.POINTER(C.c_float)]),
     "gsm_attn_aggregate": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_float,
                                      _P, _P]),
+    "gsm_render": (C.c_int, [_P, C.c_int64, C.c_int32, _P, _P, C.c_int64, _P, C.c_int32, C.c_float, C.c_float,
+                             C.c_float, C.c_float, C.c_int32, C.c_int32, C.c_int32, _P, _P]),
     "gsm_debug_set_stamps": (C.c_int, [_P, _P]),
     "gsm_destroy": (C.c_int, [_P]),
     "gsm_last_error": (C.c_int, [_P, C.c_char_p, C.c_size_t]),

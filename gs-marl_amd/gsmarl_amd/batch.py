@@ -197,6 +197,14 @@ class GpuBatchEnv:
     # ------------------------------------------------- checkpoint / injection
     STATE_KEYS = ("pos", "vel", "step_count", "episode", "ep_acc", "ep_last")
 
+    def render(self, env_ids=(0,), width: int = 700, height: int = 700, edges: bool = True) -> torch.Tensor:
+        """RGB frames uint8 [n, H, W, 3] of the current state of envs
+        ``env_ids`` (gsmarl_amd.render; camera [-L, L]^2 of each env)."""
+        from .render import render_frames
+        c = self.cfg
+        return render_frames(self.t["node_feat"], self.t["edge_ptr"], self.t["edge_index"], env_ids, width, height,
+                             (c.agent_size, c.goal_size, c.obstacle_size), c.world_half or 0.0, edges)
+
     def get_state(self) -> dict:
         return {k: self.t[k].clone() for k in self.STATE_KEYS}
 

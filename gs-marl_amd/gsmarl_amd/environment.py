@@ -142,6 +142,16 @@ class MultiAgentEnv:
         return dict(node_feat=o["node_feat"].reshape(-1, 7), edge_index=o["edge_index"],
                     edge_attr=o["edge_attr"], edge_ptr=o["edge_ptr"])
 
+    def render(self, mode: str = "rgb_array", env_ids=(0,), width: int = 700, height: int = 700,
+               edges: bool = True):
+        """MPE ``render``: one RGB frame (uint8 [H, W, 3] NumPy array) per env
+        of ``env_ids``, drawn on the GPU from the current node features and
+        edges (gsmarl_amd.render). Only ``rgb_array`` (there is no display)."""
+        if mode != "rgb_array":
+            raise NotImplementedError("only mode='rgb_array' (no window system)")
+        frames = self.batch.render(env_ids, width=width, height=height, edges=edges)
+        return list(frames.cpu().numpy())
+
     def close(self):
         self.batch.close()
 

@@ -165,6 +165,19 @@ class GraphRolloutBuffer:
                     batch=torch.arange(K, device=t.device).repeat_interleave(E),
                     ptr=ptr)
 
+    def render(self, env: int = 0, slots=None, width: int = 700, height: int = 700,
+               edges: bool = True) -> torch.Tensor:
+        """Frames uint8 [len(slots), H, W, 3] of env ``env`` over the stored
+        slots (default: all T+1), straight from the buffer (gsmarl_amd.render);
+        ``gsmarl_amd.render.save_gif`` writes them out."""
+        from .render import render_frames
+        c = self.env.cfg
+        slots = range(self.T + 1) if slots is None else slots
+        frames = [render_frames(self.node_feat[t], self.edge_ptr[t], self.edge_index[t], [env], width, height,
+                                (c.agent_size, c.goal_size, c.obstacle_size), c.world_half or 0.0, edges)
+                  for t in slots]
+        return torch.cat(frames)
+
     def compute_returns(self, values: torch.Tensor, gamma: float = 0.99, gae_lambda: float = 0.95,
                         which: str = "reward") -> torch.Tensor:
         """GAE returns [T, B, N] of the rewards (or costs, for the safe-RL

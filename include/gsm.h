@@ -32,7 +32,8 @@
 extern "C" {
 #endif
 
-#define GSM_ABI_VERSION 3
+/* 4: lagged-emission graph chains (GSM_GRAPH_UNFUSED / _LAG_ONLY), gsm_render */
+#define GSM_ABI_VERSION 4
 
 typedef enum gsm_status {
     GSM_OK = 0,
@@ -237,6 +238,24 @@ int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_mean_ms, float 
 int gsm_attn_aggregate(const float *q, const float *k, const float *v, const float *edge_w, const float *w_e,
                        const int64_t *row_ptr, const int32_t *col, const float *skip, int64_t n_nodes,
                        int32_t heads, int32_t channels, float scale, float *out, void *stream);
+
+/* Episode frames (replaces the pyglet viewer of
+ * multiagent/rendering.py, SOURCES.txt:18, used by scripts/render_mpe.py,
+ * SOURCES.txt:30, for the demo/ GIFs, readme.md:64). Draws env env_ids[f]
+ * of a batch into frame f of rgba (uint8 [n_frames][height][width][4]) from
+ * its node-feature rows (node_feat: f32 [n_envs][n_entities][7], position in
+ * columns 2-3, type 0 agent / 1 goal-target / 2 obstacle / -1 padding in
+ * column 6) and, with GSM_RENDER_EDGES, its packed CSR edges (edge_ptr int64
+ * [n_envs+1], edge_index int32 [2][edge_capacity], global ids b*n_entities+e)
+ * as black lines. Camera [-L, L]^2 with L = half_width, or sqrt(n_agents/3)
+ * of the env when half_width <= 0; disc radii = the three sizes. Any rollout
+ * slot can be rendered. Out-of-range env ids give white frames. Stateless;
+ * asynchronous on `stream`. */
+#define GSM_RENDER_EDGES 1
+int gsm_render(const float *node_feat, int64_t n_envs, int32_t n_entities, const int64_t *edge_ptr,
+               const int32_t *edge_index, int64_t edge_capacity, const int32_t *env_ids, int32_t n_frames,
+               float half_width, float agent_size, float target_size, float obstacle_size, int32_t width,
+               int32_t height, int32_t flags, uint8_t *rgba, void *stream);
 
 /* Diagnostics: device buffer (uint64 [2 * n_blocks * 4][16]) that libraries
  * built with -DGSM_STAMPS fill with per-wave phase timestamps; ignored by the
