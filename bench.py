@@ -78,12 +78,18 @@ def emit_kernel_bytes(B, N, No, total_edges, seg=True):
     return B * per_env + 12 * total_edges
 
 
-def lag_extra_bytes(B, N, No, total_edges):
+def lag_extra_bytes(B, N, No, total_edges, seg=True):
     """Bytes a lagged step kernel moves on top of step_kernel_bytes: the
     previous step's emission minus what the step part already reads (entity
-    positions, obstacle row masks) — the agent row masks, edge count, the
-    edge_ptr entry and 12 B per edge."""
-    return B * (8 * N + 4 + 8) + 12 * total_edges
+    positions, the obstacle rows' cached words) — the rest of the row masks,
+    the env's edge sum, the edge_ptr entry and 12 B per edge."""
+    M = N + No
+    if seg:
+        masks = 8 * N
+    else:
+        W, ka = (M + 63) // 64, (N + 63) // 64
+        masks = 8 * (M * W - No * (W - ka))
+    return B * (masks + 4 + 8) + 12 * total_edges
 
 
 def ragged_kernel_bytes(env, EL, action_bytes, total_edges):
@@ -343,10 +349,10 @@ def main():
         else:
             sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4, seg)
             if lag:
-                sb += lag_extra_bytes(B, N, cfg.n_obstacles, edges_now)
+                sb += lag_extra_bytes(B, N, cfg.n_obstacles, edges_now, seg)
             eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)
-            names = (("gsm_step_seg_kernel<lagged emission>" if lag else "gsm_step_seg_kernel"),
-                     "gsm_emit_seg_kernel") if seg else ("gsm_step_tile_kernel", "gsm_emit_tile_kernel")
+            fam = "seg" if seg else "tile"
+            names = (f"gsm_step_{fam}_kernel" + ("<lagged emission>" if lag else ""), f"gsm_emit_{fam}_kernel")
         kern = {"step": dict(kernel=names[0], ms=step_ms, bytes=sb, gbs=sb / (step_ms * 1e-3) / 1e9),
                 "emit": dict(kernel=names[1], ms=emit_ms, bytes=eb, gbs=eb / (emit_ms * 1e-3) / 1e9)}
         # a lagged chain runs the emit kernel once per graph, the step kernel every step

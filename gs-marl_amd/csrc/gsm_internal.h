@@ -87,7 +87,8 @@ const void *step_kernel_fn(const DevParams &p);
 const void *emit_kernel_fn(const DevParams &p);
 const void *step_seg_kernel_fn(const DevParams &p);
 // step kernel that emits the previous step's edges first (p.lag); nullptr
-// where the path has none (tile, ragged)
+// where the path has none (tile: measured no faster than its own emit
+// launch; ragged)
 const void *lag_step_kernel_fn(const DevParams &p);
 const void *lag_step_seg_kernel_fn(const DevParams &p);
 const void *emit_seg_kernel_fn(const DevParams &p);

@@ -12,7 +12,7 @@
 //   ragged     polygon / line / mixed: one wave per env, per-env shape,
 //              per-step assignment (gsm_ragged_kernels.hip).
 //
-// Inside a graph chain the segmented family can fuse the emitter of step t
+// Inside a graph chain the segmented family fuses the emitter of step t
 // into the step kernel of step t+1 ("lagged emission"): the
 // edges of step t are functions of the positions and row masks that step t+1
 // loads anyway, so the chain is step_0, lag_step_1, ..., lag_step_{T-1},

@@ -175,6 +175,86 @@ __device__ __forceinline__ int obs_sweep_any(const DevParams &p, const float2 *s
 #else
 #define GSM_TILE_ATTR
 #endif
+// ---------------------------------------------------------------------------
+// edge emitter
+// ---------------------------------------------------------------------------
+// Row r's edges in entity order from its radius mask words: agent rows ->
+// agents, own goal (always), obstacles; goal rows -> own agent; obstacle rows
+// -> agents, obstacles. kWrite = false only counts.
+template <bool kWrite>
+__device__ __forceinline__ int row_edges(const DevParams &p, const EdgeSink &out, const float2 *s_pos,
+                                         const uint64_t *rmask, int r, int64_t off, int32_t g0) {
+    const int N = p.N, W = p.W;
+    if (r >= N && r < 2 * N) {   // goal row: goal i -> agent i
+        if (kWrite && off < out.cap) {
+            const float2 a = s_pos[r], q = s_pos[r - N];
+            const float dx = a.x - q.x, dy = a.y - q.y;
+            out.index[off] = g0 + r;
+            out.index[out.cap + off] = g0 + r - N;
+            out.attr[off] = sqrtf(dx * dx + dy * dy);
+        }
+        return 1;
+    }
+    const int m = r < N ? r : r - N;             // collider row
+    const uint64_t *row = rmask + (int64_t)m * W;
+    if (!kWrite) {
+        int n = r < N ? 1 : 0;
+        for (int k = 0; k < W; ++k) n += __popcll(row[k]);
+        return n;
+    }
+    const float2 a = s_pos[r];
+    int n = 0;
+    auto put = [&](int dst) {
+        if (off + n < out.cap) {   // redirected outputs may be smaller than the worst case
+            const float2 q = s_pos[dst];
+            const float dx = a.x - q.x, dy = a.y - q.y;
+            out.index[off + n] = g0 + r;
+            out.index[out.cap + off + n] = g0 + dst;
+            out.attr[off + n] = sqrtf(dx * dx + dy * dy);
+        }
+        ++n;
+    };
+    bool goal_done = r >= N;
+    for (int k = 0; k < W; ++k) {
+        uint64_t bits = row[k];
+        while (bits) {
+            const int c = 64 * k + __builtin_ctzll(bits);
+            bits &= bits - 1;
+            if (!goal_done && c >= N) {   // own goal sits between agents and obstacles
+                put(N + r);
+                goal_done = true;
+            }
+            put(collider_entity(c, N));
+        }
+    }
+    if (!goal_done) put(N + r);
+    return n;
+}
+
+// Env b's edges at global offset `off` (workgroup-wide: barriers): each
+// thread takes a contiguous run of rows, counts them from the mask words, a
+// workgroup scan gives the run offsets, then the runs are written. s_red:
+// kTileWaves ints.
+__device__ __forceinline__ void emit_env(const DevParams &p, const EdgeSink &out, const float2 *s_pos,
+                                         const uint64_t *rmask, int64_t off, int *s_red) {
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int E = p.E;
+    const int R = (E + kTileBlock - 1) / kTileBlock;
+    const int r0 = tid * R, r1 = min(E, r0 + R);
+    const int32_t g0 = (int32_t)((int64_t)blockIdx.x * E);
+    int mine = 0;
+    for (int r = r0; r < r1; ++r) mine += row_edges<false>(p, out, s_pos, rmask, r, 0, g0);
+    const int incl = wave_scan(mine);
+    __syncthreads();
+    if (lane == 63) s_red[wave] = incl;
+    __syncthreads();
+    int base = incl - mine;
+    for (int w = 0; w < wave; ++w) base += s_red[w];
+    int64_t o = off + base;
+    for (int r = r0; r < r1; ++r) o += row_edges<true>(p, out, s_pos, rmask, r, o, g0);
+    __syncthreads();   // s_red is reused by the caller
+}
+
 __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int b = blockIdx.x;
@@ -363,91 +443,21 @@ skip_nf:
     }
 }
 
-// ---------------------------------------------------------------------------
-// edge emitter
-// ---------------------------------------------------------------------------
-// Row r's edges in entity order from its radius mask words: agent rows ->
-// agents, own goal (always), obstacles; goal rows -> own agent; obstacle rows
-// -> agents, obstacles. kWrite = false only counts.
-template <bool kWrite>
-__device__ __forceinline__ int row_edges(const DevParams &p, const float2 *s_pos, const uint64_t *rmask, int r,
-                                         int64_t off, int32_t g0) {
-    const int N = p.N, W = p.W;
-    if (r >= N && r < 2 * N) {   // goal row: goal i -> agent i
-        if (kWrite && off < p.edge_capacity) {
-            const float2 a = s_pos[r], q = s_pos[r - N];
-            const float dx = a.x - q.x, dy = a.y - q.y;
-            p.edge_index[off] = g0 + r;
-            p.edge_index[p.edge_capacity + off] = g0 + r - N;
-            p.edge_attr[off] = sqrtf(dx * dx + dy * dy);
-        }
-        return 1;
-    }
-    const int m = r < N ? r : r - N;             // collider row
-    const uint64_t *row = rmask + (int64_t)m * W;
-    if (!kWrite) {
-        int n = r < N ? 1 : 0;
-        for (int k = 0; k < W; ++k) n += __popcll(row[k]);
-        return n;
-    }
-    const float2 a = s_pos[r];
-    int n = 0;
-    auto put = [&](int dst) {
-        if (off + n < p.edge_capacity) {   // redirected outputs may be smaller than the worst case
-            const float2 q = s_pos[dst];
-            const float dx = a.x - q.x, dy = a.y - q.y;
-            p.edge_index[off + n] = g0 + r;
-            p.edge_index[p.edge_capacity + off + n] = g0 + dst;
-            p.edge_attr[off + n] = sqrtf(dx * dx + dy * dy);
-        }
-        ++n;
-    };
-    bool goal_done = r >= N;
-    for (int k = 0; k < W; ++k) {
-        uint64_t bits = row[k];
-        while (bits) {
-            const int c = 64 * k + __builtin_ctzll(bits);
-            bits &= bits - 1;
-            if (!goal_done && c >= N) {   // own goal sits between agents and obstacles
-                put(N + r);
-                goal_done = true;
-            }
-            put(collider_entity(c, N));
-        }
-    }
-    if (!goal_done) put(N + r);
-    return n;
-}
-
 __global__ __launch_bounds__(kTileBlock) void gsm_emit_tile_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int b = blockIdx.x;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x;
     const int E = p.E;
     float2 *s_pos = (float2 *)smem;
     int *s_red = (int *)(s_pos + E);          // [kTileWaves]
     const int64_t eb = b;
-    const uint64_t *rmask = p.row_mask + eb * p.M * p.W;
     // global offset: edges of envs [0, b)  (host keeps totals < 2^31)
     int before = 0;
     for (int k = tid; k < b; k += kTileBlock) before += p.edge_count[k];
     for (int e = tid; e < E; e += kTileBlock) s_pos[e] = p.pos[eb * E + e];
     const int64_t off = tile_sum(before, s_red);
-    // this thread's rows: a contiguous run (row-major order across the workgroup)
-    const int R = (E + kTileBlock - 1) / kTileBlock;
-    const int r0 = tid * R, r1 = min(E, r0 + R);
-    const int32_t g0 = (int32_t)(eb * E);
-    int mine = 0;
-    for (int r = r0; r < r1; ++r) mine += row_edges<false>(p, s_pos, rmask, r, 0, g0);
-    // workgroup exclusive scan of the per-thread counts
-    const int incl = wave_scan(mine);
-    __syncthreads();
-    if (lane == 63) s_red[wave] = incl;
-    __syncthreads();
-    int base = incl - mine;
-    for (int w = 0; w < wave; ++w) base += s_red[w];
-    int64_t o = off + base;
-    for (int r = r0; r < r1; ++r) o += row_edges<true>(p, s_pos, rmask, r, o, g0);
+    emit_env(p, EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity}, s_pos, p.row_mask + eb * p.M * p.W, off,
+             s_red);
     if (tid == 0) {
         p.edge_ptr[b] = off;
         if (b == p.B - 1) p.edge_ptr[p.B] = off + p.edge_count[b];

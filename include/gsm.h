@@ -203,7 +203,7 @@ int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream);
  * allocates one n_blocks int32 buffer for this on first use).
  * GSM_GRAPH_UNFUSED forces the two-kernel chain (TIME_EACH implies it);
  * GSM_GRAPH_LAG_ONLY builds n_steps lagged step kernels and nothing else
- * (a timing tool: the last step's edges are left unemitted).
+ * (a timing tool: the last step's edges are left unemitted; segmented only).
  * Graphs are dropped by gsm_bind and by a reseed to a different seed. */
 #define GSM_GRAPH_SLOTS 4
 #define GSM_GRAPH_STEP 1

@@ -259,12 +259,14 @@ def test_graph_replay_equals_eager_and_deterministic():
     assert torch.equal(eager["pos"], env.t["pos"])
 
 
-@pytest.mark.parametrize("N,B,T", [(24, 256, 40), (24, 257, 7), (3, 4000, 1), (3, 123, 2), (5, 37, 9), (7, 64, 6)])
+@pytest.mark.parametrize("N,B,T", [(24, 256, 40), (24, 257, 7), (3, 4000, 1), (3, 123, 2), (5, 37, 9), (7, 64, 6),
+                                   (70, 9, 3), (96, 17, 6)])
 def test_lagged_chain_equals_eager(N, B, T):
     """Segmented graphs emit step j's edges from step j+1's kernel (lagged
     emission): the chain must leave every state and output buffer exactly as
     eager steps and as the two-kernel chain do, for odd and even chain
-    lengths, partial workgroups and auto-resets (episode length 5)."""
+    lengths, partial workgroups and auto-resets (episode length 5). Tile
+    shapes (M > 64) run the two-kernel chain under both names."""
     env, ocfg = _env(n_agents=N, n_envs=B, episode_length=5)
     acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
     keys = ("pos", "vel", "step_count", "episode", "node_feat", "reward", "cost", "done", "edge_count",
@@ -295,12 +297,13 @@ def test_lagged_chain_equals_eager(N, B, T):
     env.close()
 
 
-def test_lag_only_graph():
+@pytest.mark.parametrize("N,B", [(24, 300), (5, 41)])
+def test_lag_only_graph(N, B):
     """The lagged-kernel timing graph: physics like eager steps; its last
     emission is that of the step before the last."""
-    env, ocfg = _env(n_agents=24, n_envs=300, episode_length=1000)
+    env, ocfg = _env(n_agents=N, n_envs=B, episode_length=1000)
     T = 6
-    acts = torch.randint(0, 5, (T, 300, 24), dtype=torch.int32, device=DEV)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
     env.reset(seed=9)
     for t in range(T - 1):
         env.step(acts[t], sync_edges=False)

@@ -17,11 +17,8 @@ for c in c2 c3 c4; do
   timeout -k 10 300 python bench.py --config $c --cpu-seconds 10 > $O/bench_$c.json 2> $O/bench_$c.err || { tail -20 $O/bench_$c.err; exit 5; }
 done
 cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof" -o run --output-format csv -- python "$GRAFT_REPO_ROOT/bench.py" --no-cpu-baseline > "$GRAFT_REPO_ROOT/$O/prof.log" 2>&1 || exit 6
-cd "$GRAFT_REPO_ROOT" && for c in c3 c4; do
+cd "$GRAFT_REPO_ROOT" && for c in c2 c3 c4; do
   cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof_$c" -o run --output-format csv -- python "$GRAFT_REPO_ROOT/bench.py" --config $c --no-cpu-baseline > "$GRAFT_REPO_ROOT/$O/prof_$c.log" 2>&1 || exit 7
 done
-cd "$GRAFT_REPO_ROOT" && python - <<'PY'
-import json, glob, os
-O = os.environ.get("O_DIR")
-PY
+cd "$GRAFT_REPO_ROOT" && timeout -k 10 300 python bench.py --unfused --no-cpu-baseline > $O/bench_h_unfused.json 2> $O/bench_h_unfused.err || exit 8
 echo done
