@@ -144,6 +144,10 @@ __device__ __forceinline__ float2 slot_of(const DevParams &p, const RShape &s, i
 // lane's column (row `lane`), and its cost in *own.
 __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, float *own) {
     const bool col = lane < N;
+#ifdef GSM_ABL_NO_LSA   // timing-only ablation: identity assignment
+    *own = 0.0f;
+    return col ? lane : -1;
+#endif
     for (int i = 0; i < N; ++i) {
         const float2 pi = rl_f2(pa, i);
         if (col) {
