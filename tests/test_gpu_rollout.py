@@ -95,6 +95,36 @@ def test_edge_overflow_is_truncated():
     ref.close()
 
 
+@pytest.mark.parametrize("N,B", [(24, 32), (3, 50)])
+def test_graph_chain_overflow_is_truncated(N, B):
+    """A lagged graph chain into slots far too small: every slot keeps its
+    true CSR offsets and exactly the prefix of edges that fits; no slot's
+    emission spills into another slot (each is checked against a plain env)."""
+    from gsmarl_amd import GraphRolloutBuffer
+    env, ref = _pair(n_agents=N, n_envs=B, seed=6, episode_length=3)
+    T = 5
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    buf = GraphRolloutBuffer(env, episode_length=T, edges_per_env=2)
+    buf.reset(seed=6)
+    buf.capture(acts)
+    buf.replay()
+    outs = [ref.reset(seed=6)]
+    outs[0] = {k: v.clone() for k, v in outs[0].items()}
+    for t in range(T):
+        o = ref.step(acts[t])
+        outs.append({k: v.clone() for k, v in o.items()})
+    torch.cuda.synchronize()
+    assert bool(buf.overflowed())
+    cap = buf.cap
+    for t in range(T + 1):
+        assert torch.equal(buf.edge_ptr[t], outs[t]["edge_ptr"]), t
+        assert torch.equal(buf.edge_index[t][0], outs[t]["edge_index"][0, :cap]), t
+        assert torch.equal(buf.edge_index[t][1], outs[t]["edge_index"][1, :cap]), t
+        assert torch.equal(buf.edge_attr[t], outs[t]["edge_attr"][:cap]), t
+    env.close()
+    ref.close()
+
+
 def test_graph_batch_and_returns():
     from gsmarl_amd import GraphRolloutBuffer
     from gsmarl_amd import EnvConfig, GpuBatchEnv
