@@ -135,12 +135,15 @@ __device__ __forceinline__ float2 action_force(const DevParams &p, int64_t a) {
 // dominant term max(D, 0) is exact and the transcendental part is a
 // correction < k*ln2, so the hardware v_exp/v_log/v_rcp/v_sqrt (<= 1 ulp)
 // keep |F| within ~2e-7 relative (positions/velocities stay within the 1e-6
-// parity bar).
+// parity bar). The raw base-2 v_exp_f32 / v_log_f32 are used
+// directly: 1 + e lies in (1, 2], so the library log's denormal scaling
+// (a dozen VALU per pair) is never needed, and an exp2 underflow is e = 0.
 __device__ __forceinline__ float contact_scale(const DevParams &p, float d2, float dmin) {
+    constexpr float kLog2e = 1.44269504088896341f, kLn2 = 0.693147180559945309f;
     const float d = __builtin_amdgcn_sqrtf(d2);
     const float D = dmin - d;
-    const float e = __expf(-fabsf(D) * p.inv_k);                 // in (0, 1]
-    const float pen = fmaxf(D, 0.0f) + p.k * __logf(1.0f + e);
+    const float e = __builtin_amdgcn_exp2f(-fabsf(D) * (p.inv_k * kLog2e));   // in [0, 1]
+    const float pen = fmaxf(D, 0.0f) + (p.k * kLn2) * __builtin_amdgcn_logf(1.0f + e);
     return p.cf * pen * __builtin_amdgcn_rcpf(d);
 }
 

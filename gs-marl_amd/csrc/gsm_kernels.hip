@@ -45,9 +45,13 @@ const void *emit_kernel_fn(const DevParams &p) {
     if (p.path == kPathTile) return emit_tile_kernel_fn();
     return emit_seg_kernel_fn(p);
 }
+#ifndef GSM_LDS_PAD   // experiment: extra LDS per segmented step workgroup (caps residency)
+#define GSM_LDS_PAD 0
+#endif
 size_t step_kernel_lds(const DevParams &p) {
     // segmented: + per-wave edge sums and (lagged emission) per-wave prefix words
-    return p.path == kPathTile ? (size_t)p.wave_lds_step : (size_t)kWavesPerBlock * p.wave_lds_step + 32;
+    return p.path == kPathTile ? (size_t)p.wave_lds_step
+                               : (size_t)kWavesPerBlock * p.wave_lds_step + 32 + GSM_LDS_PAD;
 }
 size_t emit_kernel_lds(const DevParams &p) {
     return p.path == kPathTile ? (size_t)p.wave_lds_emit : (size_t)kWavesPerBlock * p.wave_lds_emit + 16;

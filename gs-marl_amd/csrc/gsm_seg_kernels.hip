@@ -145,6 +145,129 @@ __device__ __forceinline__ T seg_total(T v, const Lane &L, int M) {
 template <int kN>
 using OwnBits = typename std::conditional<(kN > 0 && kN <= 32), uint32_t, uint64_t>::type;
 
+// 2*own + (this lane's bit of `lanes`): one v_addc per column (the compiler
+// builds own |= bit << j from a select and a shift-or)
+__device__ __forceinline__ uint32_t shl1_add_lane(uint32_t own, uint64_t lanes) {
+    uint32_t r;
+    uint64_t co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(own), "s"(lanes));
+    return r;
+}
+
+// low 16 bits of a, low 16 bits of b above them (one s_pack_ll_b32_b16)
+__device__ __forceinline__ uint32_t pack_lo16(uint64_t a, uint64_t b) {
+    uint32_t r;
+    asm("s_pack_ll_b32_b16 %0, %1, %2" : "=s"(r) : "s"((uint32_t)a), "s"((uint32_t)b));
+    return r;
+}
+
+// One env per wave (32 < M <= 64, compile-time N <= 32): the sweep with the
+// fewest instructions per agent column j.
+//   * lanes >= M carry a far-away position, so no ballot needs a segment mask;
+//   * two ballots: rad (0 < d2 <= R2) and near (d2 < cut2: the contact
+//     candidates plus the self and coincident pairs); three v_writelanes
+//     (low words; the two high words packed when M <= 48);
+//   * obstacle rows accumulate their agent bits with one v_addc per column
+//     (column order reversed, so one v_bfrev at the end);
+//   * collisions (d2 < dmin2 implies d2 < cut2) are counted afterwards by a
+//     walk over each agent row's near bits, which also drops the self and
+//     coincident pairs from the stored contact candidates (0 < d2 < cut2).
+template <int kN, int kNo>
+__device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, const float2 *sp, float2 pm,
+                                             bool full, uint64_t oo, uint64_t &row, uint64_t &cand, int &ccnt) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    constexpr int N = kN, M = kN + kNo;
+    static_assert(M > 32 && M <= 64 && N <= 32, "one env per wave, agent bits in the low word");
+    constexpr bool kPack = M <= 48;
+    constexpr uint64_t abits = (1ull << N) - 1;
+    const bool obst = L.live && L.m >= N;
+    if (!L.live) pm = make_float2(1.0e18f, 1.0e18f);        // d2 ~ 1e36: every predicate false
+    const f32x2 pv = {pm.x, pm.y};
+    const uint32_t r2b = __float_as_uint(p.R2);
+    const uint32_t nearb = __float_as_uint(obst ? p.cut2_ao : p.cut2_aa);
+    const uint64_t r0 = (!full && obst) ? (oo & ~abits) : 0ull;
+    uint32_t r_lo = (uint32_t)r0, r_hi = (uint32_t)(r0 >> 32);
+    uint32_t c_lo = 0, c_hi = 0, hi = kPack ? (r_hi & 0xffffu) : 0u;
+    uint32_t own = 0;                                       // bit N-1-j = rad(lane, j)
+    auto column = [&](int j, f32x2 q) {
+        const f32x2 d = pv - q;
+        const f32x2 sq = d * d;
+        const float d2 = sq.x + sq.y;
+        const uint32_t bd = __float_as_uint(d2);
+        const uint64_t b_rad = __ballot(bd - 1u < r2b);
+        const uint64_t b_near = __ballot(bd < nearb);
+        own = shl1_add_lane(own, b_rad);
+        r_lo = writelane_u32((uint32_t)b_rad, (uint32_t)j, r_lo);
+        c_lo = writelane_u32((uint32_t)b_near, (uint32_t)j, c_lo);
+        if constexpr (kPack) {
+            hi = writelane_u32(pack_lo16(b_rad >> 32, b_near >> 32), (uint32_t)j, hi);
+        } else {
+            r_hi = writelane_u32((uint32_t)(b_rad >> 32), (uint32_t)j, r_hi);
+            c_hi = writelane_u32((uint32_t)(b_near >> 32), (uint32_t)j, c_hi);
+        }
+    };
+    // columns in groups of kU, the next group's positions read from LDS
+    // while this group is processed (a single wave otherwise waits out the
+    // LDS latency once per group)
+    constexpr int kU = 4;
+    f32x2 qn[kU];
+#pragma unroll
+    for (int u = 0; u < kU; ++u) qn[u] = *(const f32x2 *)(sp + (u < N ? u : N - 1));
+    for (int j0 = 0; j0 < N; j0 += kU) {
+        f32x2 q[kU];
+#pragma unroll
+        for (int u = 0; u < kU; ++u) q[u] = qn[u];
+        if (j0 + kU < N) {
+#pragma unroll
+            for (int u = 0; u < kU; ++u) {
+                const int jn = j0 + kU + u;
+                qn[u] = *(const f32x2 *)(sp + (jn < N ? jn : N - 1));
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < kU; ++u)
+            if (N % kU == 0 || j0 + u < N) column(j0 + u, q[u]);
+    }
+    own = __builtin_bitreverse32(own) >> (32 - N);
+    if constexpr (kPack) {
+        r_hi = hi & 0xffffu;
+        c_hi = hi >> 16;
+    }
+    uint64_t r = ((uint64_t)r_hi << 32) | r_lo;
+    uint64_t near = ((uint64_t)c_hi << 32) | c_lo;
+    if (obst) r = (r & ~abits) | own;                       // agent bits of obstacle rows
+    if (full) {
+        // obstacle columns: obstacle-obstacle bits (the agent-obstacle bits
+        // of agent rows were captured above)
+#pragma unroll 2
+        for (int k = N; k < M; ++k) {
+            const float2 q = sp[N + k];
+            const float dx = pm.x - q.x, dy = pm.y - q.y;
+            const float d2 = dx * dx + dy * dy;
+            if (obst && d2 > 0.0f && d2 <= p.R2) r |= 1ull << k;
+        }
+    }
+    // collisions and contact candidates of agent rows from the near bits
+    int cc = 0;
+    uint64_t c = 0;
+    if (L.agent) {
+        uint64_t w = near & ~(1ull << L.m);
+        c = w;
+        while (w) {
+            const int k = __builtin_ctzll(w);
+            w &= w - 1;
+            const float2 q = sp[k < N ? k : N + k];
+            const float dx = pm.x - q.x, dy = pm.y - q.y;
+            const float d2 = dx * dx + dy * dy;
+            cc += d2 < (k < N ? p.dmin2_aa : p.dmin2_ao) ? 1 : 0;
+            if (d2 == 0.0f) c &= ~(1ull << k);
+        }
+    }
+    row = r;
+    cand = c;
+    ccnt = cc;
+}
+
 // Observation sweep (file header). row/cand/ccnt are per lane: row = radius
 // row mask (compact bits), cand = contact candidates (agent lanes),
 // ccnt = collisions of agent lanes (self excluded). With full = false the
@@ -153,6 +276,10 @@ template <int kN, int kNo, int kG>
 __device__ __forceinline__ void obs_sweep(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L,
                                           const float2 *sp, float2 pm, bool full, uint64_t oo,
                                           uint64_t &row, uint64_t &cand, int &ccnt) {
+    if constexpr (kG == 1 && kN > 0 && kN <= 32 && kN + kNo > 32) {
+        obs_sweep_g1<kN, kNo>(p, L, sp, pm, full, oo, row, cand, ccnt);
+        return;
+    }
     const int N = s.N, M = s.M;
     const uint64_t segmask = M >= 64 ? ~0ull : ((1ull << M) - 1);
     const uint64_t abits = N >= 64 ? ~0ull : ((1ull << N) - 1);
@@ -292,7 +419,30 @@ __device__ __forceinline__ void emit_rows(const Shape<kN, kNo> &s, const Lane &L
             const float dx = pm.x - q.x, dy = pm.y - q.y;
             put(o++, gs, col, __builtin_amdgcn_sqrtf(dx * dx + dy * dy));
         };
-        if constexpr (kN > 0 && kN <= 32 && kNo <= 32) {
+        if constexpr (kG == 1 && kN > 0 && kN <= 32 && kN + kNo > 32) {
+            // one walk over the whole row (its length is the longest row of
+            // the wave, not the longest agent part plus the longest obstacle
+            // part); an agent row's own-goal edge sits between its agent and
+            // obstacle columns, so columns >= N shift by one
+            const uint32_t gshift = L.agent ? 1u : 0u;
+            if (L.agent) {
+                const float2 q = s_pos[N + m];
+                const float dx = pm.x - q.x, dy = pm.y - q.y;
+                put(o + (uint32_t)__popcll(mask & agent_bits), gs, g0 + N + m,
+                    __builtin_amdgcn_sqrtf(dx * dx + dy * dy));
+            }
+            uint64_t w = mask;
+            while (w) {
+                const int j = __builtin_ctzll(w);
+                w &= w - 1;
+                const bool ob = j >= kN;
+                const int ent = ob ? kN + j : j;
+                const float2 q = s_pos[ent];
+                const float dx = pm.x - q.x, dy = pm.y - q.y;
+                put(o + (ob ? gshift : 0u), gs, g0 + ent, __builtin_amdgcn_sqrtf(dx * dx + dy * dy));
+                ++o;
+            }
+        } else if constexpr (kN > 0 && kN <= 32 && kNo <= 32) {
             // compile-time shape with both halves in 32 bits
             uint32_t lo = (uint32_t)(mask & agent_bits), hi = (uint32_t)(mask >> kN);
             while (lo) {
@@ -337,25 +487,28 @@ __device__ __forceinline__ void emit_rows(const Shape<kN, kNo> &s, const Lane &L
 struct BlockPrefix {
     int cnt_k, acc;
 };
+// Loads at clamped addresses, predicates on the values (see seg_load): the
+// first 2 * kBlock int4 words of preceding sums (2048 workgroups, 8192
+// one-env-per-wave envs) need no loop; `any16` is any >= 16-byte buffer,
+// read in place of block_sum when no whole int4 word precedes this block.
 __device__ __forceinline__ BlockPrefix block_prefix_loads(const int32_t *block_sum, const int32_t *edge_count,
-                                                          int B, int G) {
+                                                          int B, int G, const void *any16) {
     BlockPrefix r{0, 0};
-    const int lane = threadIdx.x & 63;
+    const int lane = threadIdx.x & 63, tid = threadIdx.x;
     const int first = blockIdx.x * kWavesPerBlock * G;
     const int nblk = min(kWavesPerBlock * G, B - first);
-    if (lane < nblk) r.cnt_k = edge_count[first + lane];
-#ifdef GSM_ABL_NO_PREFIX   // timing-only ablation build (wrong offsets)
-    if (false)
-#endif
-    {
-        const int nb = (int)blockIdx.x;
-        const int nb4 = nb & ~3;
-        const int4 *bs4 = (const int4 *)block_sum;
-        for (int k = threadIdx.x; 4 * k < nb4; k += kBlock) {
-            const int4 q = bs4[k];
-            r.acc += q.x + q.y + q.z + q.w;
-        }
-        if ((int)threadIdx.x < nb - nb4) r.acc += block_sum[nb4 + threadIdx.x];
+    const int ck = edge_count[first + min(lane, nblk - 1)];
+    r.cnt_k = lane < nblk ? ck : 0;
+    const int nb = (int)blockIdx.x, n4 = nb >> 2, nb4 = n4 << 2;
+    const int4 *bs4 = n4 > 0 ? (const int4 *)block_sum : (const int4 *)any16;
+    const int kc = n4 > 0 ? n4 - 1 : 0;
+    const int4 q0 = bs4[min(tid, kc)], q1 = bs4[min(tid + kBlock, kc)];
+    const int tl = block_sum[min(nb4 + tid, max(nb - 1, 0))];
+    r.acc = (tid < n4 ? q0.x + q0.y + q0.z + q0.w : 0) + (tid + kBlock < n4 ? q1.x + q1.y + q1.z + q1.w : 0) +
+            (tid < nb - nb4 ? tl : 0);
+    for (int k = tid + 2 * kBlock; k < n4; k += kBlock) {   // more than 2048 preceding workgroups
+        const int4 q = bs4[k];
+        r.acc += q.x + q.y + q.z + q.w;
     }
     return r;
 }
@@ -410,37 +563,76 @@ struct SegIn {
     uint64_t cand_prev, oo;
     int t, ep;
     float2 acc;
+    float4 araw;   // the lane's action as loaded (seg_load_finish turns it into u)
 };
 
+// Every load is unconditional, at clamped (always valid) addresses, with the
+// lane/mode predicates applied to the values afterwards: a load under a
+// divergent branch ends in a wait for its data at the branch join, which
+// serialised the state loads into several HBM round trips.
 template <int kN, int kNo, int kFmt, bool kLag>
 __device__ __forceinline__ SegIn seg_load(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L) {
+    static_assert(kN > 0 && kFmt >= 0, "compile-time shape and action format");
+    constexpr int N = kN, E = 2 * kN + kNo, M = kN + kNo;
     SegIn in;
-    in.x0 = in.x1 = in.v = in.u = make_float2(0.0f, 0.0f);
-    in.cand_prev = in.oo = 0;
-    in.t = in.ep = 0;
-    in.acc = make_float2(0.0f, 0.0f);
-    const int N = s.N, E = s.E, M = s.M;
-    if (L.b < p.B) {
-        const int64_t eb = L.b;
-        const uint32_t um = (uint32_t)L.m;
-        const float2 *pos_b = p.pos + eb * E;
-        if (L.lane < E) in.x0 = pos_b[(uint32_t)L.lane];
-        if (L.lane + kWave < E) in.x1 = pos_b[(uint32_t)(L.lane + kWave)];
-        in.t = p.step_count[L.b];
-        in.ep = p.episode[L.b];
-        in.acc = p.ep_acc[L.b];
-        if (L.agent) {
-            in.v = (p.vel + eb * N)[um];
-            if (p.mode == kModeStep) {
-                in.u = action_force_t<kFmt>(p, eb * N + um);
-                in.cand_prev = (p.contact_mask + eb * N)[um];
-            }
-        }
-        // obstacle rows: cached obstacle-obstacle bits; lagged emission: every
-        // row (the previous step's masks)
-        if (L.live && (kLag || L.m >= N) && p.mode == kModeStep) in.oo = (p.row_mask + eb * M)[um];
+    const int64_t eb = L.b < p.B ? L.b : p.B - 1;                  // wave-uniform
+    const uint32_t lane = (uint32_t)L.lane;
+    const uint32_t ma = lane < (uint32_t)N ? lane : N - 1, mm = lane < (uint32_t)M ? lane : M - 1;
+    const float2 *pos_b = p.pos + eb * E;
+    in.x0 = pos_b[lane < (uint32_t)E ? lane : E - 1];
+    in.x1 = E > kWave ? pos_b[lane + kWave < (uint32_t)E ? lane + kWave : E - 1] : make_float2(0.0f, 0.0f);
+    in.t = p.step_count[eb];
+    in.ep = p.episode[eb];
+    in.acc = p.ep_acc[eb];
+    in.v = p.vel[eb * N + ma];
+    // reset / observe launches may carry no actions: read node features instead
+    // (28 B per entity >= any action format's bytes per agent), never used
+    const bool step = p.mode == kModeStep;
+    const int64_t ai = eb * N + ma;
+    if constexpr (kFmt == 0) {
+        const float *q = (step ? (const float *)p.actions : p.node_feat) + ai * 5;
+        in.araw = make_float4(q[1], q[2], q[3], q[4]);
+    } else if constexpr (kFmt == 1) {
+        const int32_t *q = step ? (const int32_t *)p.actions : (const int32_t *)p.node_feat;
+        in.araw = make_float4(__int_as_float(q[ai]), 0.0f, 0.0f, 0.0f);
+    } else {
+        const float2 *q = step ? (const float2 *)p.actions : (const float2 *)p.node_feat;
+        const float2 a = q[ai];
+        in.araw = make_float4(a.x, a.y, 0.0f, 0.0f);
     }
+    in.cand_prev = p.contact_mask[eb * N + ma];
+    in.oo = p.row_mask[eb * M + mm];
     return in;
+}
+
+// the lane/mode predicates and the action force, once the loads are issued
+template <int kN, int kNo, int kFmt, bool kLag>
+__device__ __forceinline__ void seg_load_finish(const DevParams &p, const Lane &L, SegIn &in) {
+    const bool step = p.mode == kModeStep;
+    const float4 a = in.araw;
+    float ux, uy;
+    if constexpr (kFmt == 0) {
+        ux = a.x - a.y;
+        uy = a.z - a.w;
+    } else if constexpr (kFmt == 1) {
+        const int k = __float_as_int(a.x);
+        ux = (float)(k == 1) - (float)(k == 2);
+        uy = (float)(k == 3) - (float)(k == 4);
+    } else {
+        ux = a.x;
+        uy = a.y;
+    }
+    const bool ag_step = L.agent && step;
+    in.u = ag_step ? make_float2(ux * p.sens, uy * p.sens) : make_float2(0.0f, 0.0f);
+    in.cand_prev = ag_step ? in.cand_prev : 0ull;
+    if (!L.agent) in.v = make_float2(0.0f, 0.0f);
+    // obstacle rows: cached obstacle-obstacle bits; lagged emission: every
+    // row (the previous step's masks)
+    in.oo = (L.live && (kLag || L.m >= kN) && step) ? in.oo : 0ull;
+    if (L.b >= p.B) {
+        in.t = in.ep = 0;
+        in.acc = make_float2(0.0f, 0.0f);
+    }
 }
 
 // One env (G = 1) or one wave's G envs: everything after the loads. Returns
@@ -463,12 +655,13 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     float2 *const pos_b = p.pos + eb * E;
     float2 *const vel_b = p.vel + eb * N;
     const uint32_t um = (uint32_t)m;
-    (void)wid;
 
-    int t = in.t, ep = in.ep;
-    float2 acc = in.acc;
-    float2 v = in.v, u = in.u;
-    uint64_t cand_prev = in.cand_prev, oo = in.oo;
+    SegIn inf = in;
+    if constexpr (kG == 1) seg_load_finish<kN, kNo, kFmt, kLag>(p, L, inf);
+    int t = inf.t, ep = inf.ep;
+    float2 acc = inf.acc;
+    float2 v = inf.v, u = inf.u;
+    uint64_t cand_prev = inf.cand_prev, oo = inf.oo;
     if constexpr (kG == 1) {
         if (wave_live) {
             if (L.lane < E) s_pos[L.lane] = in.x0;
@@ -492,11 +685,13 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     }
     bool reset = L.live && p.mode == kModeReset && (p.env_mask == nullptr || p.env_mask[L.b] != 0);
     wave_sync();
+    GSM_STAMP(p, wid, 1);
     if constexpr (kLag) {
         // the previous step's edges: its positions (staged above) and row masks
         block_emit<kN, kNo, kG>(p, s, L, s_pos, oo, lag_pre, s_lag, p.lag.edge_ptr,
                                 EdgeSink{p.lag.edge_index, p.lag.edge_attr, p.lag.cap});
     }
+    GSM_STAMP(p, wid, 2);
 
     // scenario.reset_world (Philox layout, App. A S14) for the lanes' envs
     auto relayout = [&]() {
@@ -554,6 +749,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
         t += 1;
         done = L.live && t >= p.EL;
     }
+    GSM_STAMP(p, wid, 3);
 
     // ---- observation pass on the post-physics positions
     const bool full = p.mode != kModeStep;                  // reset / observe: recompute obstacle pairs
@@ -566,6 +762,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
 #else
     obs_sweep<kN, kNo, kG>(p, s, L, s_pos, pm, full, oo, row, cand, ccnt);
 #endif
+    GSM_STAMP(p, wid, 4);
 
     // reward / cost callbacks
     float r = 0.0f;
@@ -608,13 +805,17 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
         }
     }
     if (!L.live) row = 0;
+    GSM_STAMP(p, wid, 5);
 
     // ---- outputs and state. Node features: agent rows every step; goal and
     // obstacle rows (static within an episode) only when the layout is new or
     // on an observe. Rows are staged in LDS and stored lane-linear.
     const bool any_statics = p.mode != kModeStep || p.nf_full || __any(relaid);
+    // one env per wave: rows go straight to HBM (each lane its 28-byte row,
+    // the wave's rows contiguous); G > 1: staged in LDS, stored lane-linear
+    constexpr bool kDirectNf = kG == 1;
     if (L.live) {
-        float *nf = s_nf + segc * E * 7;
+        float *nf = kDirectNf ? p.node_feat + eb * E * 7 : s_nf + segc * E * 7;
         if (L.agent) {
             const float2 g = s_pos[N + m];
             store_row(nf + m * 7, v, pm, make_float2(g.x - pm.x, g.y - pm.y), 0.0f);
@@ -632,8 +833,8 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
         if (L.agent) (p.contact_mask + eb * N)[um] = cand;
         (p.row_mask + eb * M)[um] = row;
     }
-    wave_sync();
-    {
+    if constexpr (!kDirectNf) {
+        wave_sync();
         const int b0 = kG == 1 ? L.b : (blockIdx.x * kWavesPerBlock + L.wave) * G;
         for (int g = 0; g < G; ++g) {
             if (b0 + g >= p.B) break;
@@ -649,6 +850,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
         }
     }
 
+    GSM_STAMP(p, wid, 6);
 #ifdef GSM_ABL_FUSED_PADDED   // timing-only: emit here at a fixed per-env stride
     emit_rows<kN, kNo, kG>(s, L, s_pos, row, (int64_t)(L.live ? L.b : 0) * (p.edge_capacity / p.B),
                            EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity});
@@ -676,6 +878,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
             p.edge_count[L.b] = env_edges;
         }
     }
+    GSM_STAMP(p, wid, 7);
     return wave_edges;
 }
 
@@ -691,11 +894,12 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
     int *s_bc = (int *)(smem + kWavesPerBlock * p.wave_lds_step);
     int *s_lag = s_bc + kWavesPerBlock;
     GSM_RSTAMP(p, wid, 8);
+    GSM_STAMP(p, wid, 0);
     {
         SegIn in{};
         if constexpr (kG == 1) in = seg_load<kN, kNo, kFmt, kLag>(p, s, L);
         BlockPrefix lag_pre{0, 0};
-        if constexpr (kLag) lag_pre = block_prefix_loads(p.lag.block_sum, p.lag.edge_count, p.B, s.G);
+        if constexpr (kLag) lag_pre = block_prefix_loads(p.lag.block_sum, p.lag.edge_count, p.B, s.G, p.pos);
         const int edges = seg_env<kN, kNo, kFmt, kLag>(p, s, L, wave_lds, in, wid, lag_pre, s_lag);
         if (L.lane == 0) s_bc[wave] = edges;
         __syncthreads();
@@ -728,7 +932,7 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
 
     // every global load first (positions, row masks, the block's edge counts,
     // the preceding blocks' sums), then the first wait
-    const BlockPrefix pre = block_prefix_loads(p.block_edge_sum, p.edge_count, p.B, G);
+    const BlockPrefix pre = block_prefix_loads(p.block_edge_sum, p.edge_count, p.B, G, p.pos);
     uint64_t mask = 0;
     float2 x0 = make_float2(0.0f, 0.0f), x1 = x0;
     if constexpr (kG == 1) {

@@ -1,6 +1,9 @@
 """Per-phase wave timelines from a -DGSM_STAMPS build (tools/ablate.sh build
 "stamps:-DGSM_STAMPS"). Runs one timed 100-step graph on the headline config
-and summarises the last step's stamps (diagnostic only; stamps perturb timing)."""
+and summarises the last step's stamps (diagnostic only; stamps perturb timing).
+Step-kernel phases (gsm_seg_kernels.hip): 0 entry, 1 inputs staged, 2 lagged
+emission done, 3 physics, 4 sweep, 5 reward/cost/auto-reset, 6 node features
+and state stores, 7 counters."""
 import ctypes as C
 import json
 import os
@@ -31,7 +34,6 @@ for name, rows, phases in (("step", s[: nb * 4], 8), ("emit", s[nb * 4:], 5)):
     out[name] = dict(
         waves=int(len(live)),
         phase_cycles_median=[int(x) for x in np.median(d, axis=0)],
-        sub_3_10_11_12_4=[int(np.median(live[:, b] - live[:, a])) for a, b in ((3, 10), (10, 11), (11, 12), (12, 4))] if name == "step" else None,
         phase_cycles_mean=[int(x) for x in d.mean(axis=0)],
         wave_total_cycles_median=int(np.median(live[:, phases - 1] - live[:, 0])),
         start_spread_us=float((rt0.max() - rt0.min()) / 100.0),
