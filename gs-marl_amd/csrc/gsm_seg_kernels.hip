@@ -161,41 +161,47 @@ __device__ __forceinline__ uint32_t pack_lo16(uint64_t a, uint64_t b) {
     return r;
 }
 
-// One env per wave (32 < M <= 64, compile-time N <= 32): the sweep with the
-// fewest instructions per agent column j.
+// One env per wave (32 < M <= 64, compile-time even N <= 32): the sweep with
+// the fewest instructions per agent column j.
+//   * the agent positions are re-staged as column pairs [x_j x_j+1 y_j y_j+1]
+//     (s_xy, 16 B per pair) so one ds_read_b128 and five packed-f32 VALU give
+//     the squared distances of two columns; the next group's pairs are read
+//     while this group is processed;
 //   * lanes >= M carry a far-away position, so no ballot needs a segment mask;
-//   * two ballots: rad (0 < d2 <= R2) and near (d2 < cut2: the contact
-//     candidates plus the self and coincident pairs); three v_writelanes
-//     (low words; the two high words packed when M <= 48);
+//   * two ballots on plain float compares: rad' (d2 <= R2) and near
+//     (d2 < cut2: contact candidates plus the self and coincident pairs);
+//     three v_writelanes (low words; the two high words packed when M <= 48);
 //   * obstacle rows accumulate their agent bits with one v_addc per column
 //     (column order reversed, so one v_bfrev at the end);
-//   * collisions (d2 < dmin2 implies d2 < cut2) are counted afterwards by a
-//     walk over each agent row's near bits, which also drops the self and
-//     coincident pairs from the stored contact candidates (0 < d2 < cut2).
+//   * the walk over each agent row's near bits counts collisions
+//     (d2 < dmin2 implies d2 < cut2) and finds coincident pairs (d2 = 0);
+//     self bits are dropped, and a wave holding a coincident pair (never
+//     seen in practice) recomputes its rows with the exact 0 < d2 <= R2.
 template <int kN, int kNo>
-__device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, const float2 *sp, float2 pm,
-                                             bool full, uint64_t oo, uint64_t &row, uint64_t &cand, int &ccnt) {
+__device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, const float2 *sp, float *s_xy,
+                                             float2 pm, bool full, uint64_t oo, uint64_t &row, uint64_t &cand,
+                                             int &ccnt) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     constexpr int N = kN, M = kN + kNo;
-    static_assert(M > 32 && M <= 64 && N <= 32, "one env per wave, agent bits in the low word");
+    static_assert(M > 32 && M <= 64 && N <= 32 && N % 2 == 0, "one env per wave, agent bits in the low word");
     constexpr bool kPack = M <= 48;
     constexpr uint64_t abits = (1ull << N) - 1;
     const bool obst = L.live && L.m >= N;
+    if (L.agent) {
+        const int at = (L.m >> 1) * 4 + (L.m & 1);
+        s_xy[at] = pm.x;
+        s_xy[at + 2] = pm.y;
+    }
     if (!L.live) pm = make_float2(1.0e18f, 1.0e18f);        // d2 ~ 1e36: every predicate false
-    const f32x2 pv = {pm.x, pm.y};
-    const uint32_t r2b = __float_as_uint(p.R2);
-    const uint32_t nearb = __float_as_uint(obst ? p.cut2_ao : p.cut2_aa);
+    const float R2 = p.R2, cut2 = obst ? p.cut2_ao : p.cut2_aa;
     const uint64_t r0 = (!full && obst) ? (oo & ~abits) : 0ull;
     uint32_t r_lo = (uint32_t)r0, r_hi = (uint32_t)(r0 >> 32);
     uint32_t c_lo = 0, c_hi = 0, hi = kPack ? (r_hi & 0xffffu) : 0u;
-    uint32_t own = 0;                                       // bit N-1-j = rad(lane, j)
-    auto column = [&](int j, f32x2 q) {
-        const f32x2 d = pv - q;
-        const f32x2 sq = d * d;
-        const float d2 = sq.x + sq.y;
-        const uint32_t bd = __float_as_uint(d2);
-        const uint64_t b_rad = __ballot(bd - 1u < r2b);
-        const uint64_t b_near = __ballot(bd < nearb);
+    uint32_t own = 0;                                       // bit N-1-j = rad'(lane, j)
+    wave_sync();
+    auto column = [&](int j, float d2) {
+        const uint64_t b_rad = __ballot(d2 <= R2);
+        const uint64_t b_near = __ballot(d2 < cut2);
         own = shl1_add_lane(own, b_rad);
         r_lo = writelane_u32((uint32_t)b_rad, (uint32_t)j, r_lo);
         c_lo = writelane_u32((uint32_t)b_near, (uint32_t)j, c_lo);
@@ -206,27 +212,31 @@ __device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, 
             c_hi = writelane_u32((uint32_t)(b_near >> 32), (uint32_t)j, c_hi);
         }
     };
-    // columns in groups of kU, the next group's positions read from LDS
-    // while this group is processed (a single wave otherwise waits out the
-    // LDS latency once per group)
-    constexpr int kU = 4;
-    f32x2 qn[kU];
+    const f32x2 px = {pm.x, pm.x}, py = {pm.y, pm.y};
+    auto pair = [&](int j, float4 Q) {
+        const f32x2 dx = px - (f32x2){Q.x, Q.y};
+        const f32x2 dy = py - (f32x2){Q.z, Q.w};
+        const f32x2 d2 = dx * dx + dy * dy;
+        column(j, d2.x);
+        column(j + 1, d2.y);
+    };
+    // pairs in groups of kU, the next group read while this one is processed
+    constexpr int kP = N / 2, kU = 2;
+    const float4 *xy4 = (const float4 *)s_xy;
+    float4 qn[kU];
 #pragma unroll
-    for (int u = 0; u < kU; ++u) qn[u] = *(const f32x2 *)(sp + (u < N ? u : N - 1));
-    for (int j0 = 0; j0 < N; j0 += kU) {
-        f32x2 q[kU];
+    for (int u = 0; u < kU; ++u) qn[u] = xy4[u < kP ? u : kP - 1];
+    for (int g = 0; g < kP; g += kU) {
+        float4 q[kU];
 #pragma unroll
         for (int u = 0; u < kU; ++u) q[u] = qn[u];
-        if (j0 + kU < N) {
+        if (g + kU < kP) {
 #pragma unroll
-            for (int u = 0; u < kU; ++u) {
-                const int jn = j0 + kU + u;
-                qn[u] = *(const f32x2 *)(sp + (jn < N ? jn : N - 1));
-            }
+            for (int u = 0; u < kU; ++u) qn[u] = xy4[g + kU + u < kP ? g + kU + u : kP - 1];
         }
 #pragma unroll
         for (int u = 0; u < kU; ++u)
-            if (N % kU == 0 || j0 + u < N) column(j0 + u, q[u]);
+            if (kP % kU == 0 || g + u < kP) pair(2 * (g + u), q[u]);
     }
     own = __builtin_bitreverse32(own) >> (32 - N);
     if constexpr (kPack) {
@@ -234,8 +244,9 @@ __device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, 
         c_hi = hi >> 16;
     }
     uint64_t r = ((uint64_t)r_hi << 32) | r_lo;
-    uint64_t near = ((uint64_t)c_hi << 32) | c_lo;
+    const uint64_t near = ((uint64_t)c_hi << 32) | c_lo;
     if (obst) r = (r & ~abits) | own;                       // agent bits of obstacle rows
+    if (L.agent) r &= ~(1ull << L.m);                      // self
     if (full) {
         // obstacle columns: obstacle-obstacle bits (the agent-obstacle bits
         // of agent rows were captured above)
@@ -250,6 +261,7 @@ __device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, 
     // collisions and contact candidates of agent rows from the near bits
     int cc = 0;
     uint64_t c = 0;
+    bool coincident = false;
     if (L.agent) {
         uint64_t w = near & ~(1ull << L.m);
         c = w;
@@ -260,8 +272,24 @@ __device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, 
             const float dx = pm.x - q.x, dy = pm.y - q.y;
             const float d2 = dx * dx + dy * dy;
             cc += d2 < (k < N ? p.dmin2_aa : p.dmin2_ao) ? 1 : 0;
-            if (d2 == 0.0f) c &= ~(1ull << k);
+            if (d2 == 0.0f) {
+                c &= ~(1ull << k);
+                coincident = true;
+            }
         }
+    }
+    if (__builtin_expect(__any(coincident), 0)) {
+        // exact agent-column bits of every row (and obstacle columns of agent
+        // rows): rad' also holds coincident pairs
+        uint64_t ex = 0;
+        for (int k = 0; k < (L.agent ? M : N); ++k) {
+            const float2 q = sp[k < N ? k : N + k];
+            const float dx = pm.x - q.x, dy = pm.y - q.y;
+            const float d2 = dx * dx + dy * dy;
+            if (d2 > 0.0f && d2 <= p.R2) ex |= 1ull << k;
+        }
+        if (L.agent) r = ex;
+        else if (obst) r = (r & ~abits) | ex;
     }
     row = r;
     cand = c;
@@ -274,10 +302,10 @@ __device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, 
 // obstacle-obstacle bits are taken from `oo` (the cached masks).
 template <int kN, int kNo, int kG>
 __device__ __forceinline__ void obs_sweep(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L,
-                                          const float2 *sp, float2 pm, bool full, uint64_t oo,
+                                          const float2 *sp, float *s_xy, float2 pm, bool full, uint64_t oo,
                                           uint64_t &row, uint64_t &cand, int &ccnt) {
-    if constexpr (kG == 1 && kN > 0 && kN <= 32 && kN + kNo > 32) {
-        obs_sweep_g1<kN, kNo>(p, L, sp, pm, full, oo, row, cand, ccnt);
+    if constexpr (kG == 1 && kN > 0 && kN <= 32 && kN % 2 == 0 && kN + kNo > 32) {
+        obs_sweep_g1<kN, kNo>(p, L, sp, s_xy, pm, full, oo, row, cand, ccnt);
         return;
     }
     const int N = s.N, M = s.M;
@@ -760,7 +788,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     row = oo; cand = 0; ccnt = 0;
     asm volatile("" :: "v"(pm.x), "v"(pm.y));
 #else
-    obs_sweep<kN, kNo, kG>(p, s, L, s_pos, pm, full, oo, row, cand, ccnt);
+    obs_sweep<kN, kNo, kG>(p, s, L, s_pos, s_nf, pm, full, oo, row, cand, ccnt);
 #endif
     GSM_STAMP(p, wid, 4);
 
@@ -795,7 +823,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
             const float2 pm2 = s_pos[row_entity(m, N)];
             uint64_t row2, cand2;
             int cc2;
-            obs_sweep<kN, kNo, kG>(p, s, L, s_pos, pm2, true, 0ull, row2, cand2, cc2);
+            obs_sweep<kN, kNo, kG>(p, s, L, s_pos, s_nf, pm2, true, 0ull, row2, cand2, cc2);
             if (reset) {
                 pm = pm2;
                 row = row2;
