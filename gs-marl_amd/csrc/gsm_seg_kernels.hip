@@ -508,6 +508,52 @@ __device__ __forceinline__ void emit_rows(const Shape<kN, kNo> &s, const Lane &L
     else walk(std::false_type{});
 }
 
+// One env per wave (compile-time shape, N <= 31 agent bits and <= 32
+// obstacle bits): the env's edge list is first expanded into LDS as
+// (source entity | destination entity << 8) words in CSR order — per lane a
+// few instructions per set bit of its row, so the row-length imbalance across
+// lanes costs little — then written by all 64 lanes, edge e by lane e mod 64:
+// distances from the staged positions and three coalesced stores per 64 edges.
+template <int kN, int kNo>
+__device__ __forceinline__ void emit_rows_staged(const Lane &L, const float2 *s_pos, uint32_t *s_scr,
+                                                 uint64_t mask, int64_t env_off, const EdgeSink &out) {
+    constexpr int N = kN, E = 2 * kN + kNo;
+    static_assert(N <= 31 && kNo <= 32, "agent and obstacle column bits in one word each");
+    const int m = L.m;
+    const uint64_t mk = L.live ? mask : 0ull;
+    const uint32_t lo = (uint32_t)mk & ((1u << N) - 1u), hi = (uint32_t)(mk >> N);
+    const int c = __popc(lo) + __popc(hi) + (L.agent ? 1 : 0);
+    const int incl = wave_scan(c);
+    const int a_total = __builtin_amdgcn_readlane(incl, N - 1);
+    const int total = __builtin_amdgcn_readlane(incl, 63) + N;
+    uint32_t *at = s_scr + (incl - c + (m >= N ? N : 0));
+    const uint32_t src = (uint32_t)row_entity(m, N);
+    for (uint32_t w = lo; w; w &= w - 1) *at++ = src | ((uint32_t)__builtin_ctz(w) << 8);
+    if (L.agent) {
+        *at++ = src | ((uint32_t)(N + m) << 8);             // agent m -> its goal
+        s_scr[a_total + m] = (uint32_t)(N + m) | ((uint32_t)m << 8);   // goal row
+    }
+    for (uint32_t w = hi; w; w &= w - 1) *at++ = src | ((uint32_t)(2 * N + __builtin_ctz(w)) << 8);
+    wave_sync();
+    const int64_t eb = L.b;
+    const int32_t g0 = (int32_t)(eb * E);
+    const uint32_t wb_lo = __builtin_amdgcn_readfirstlane((uint32_t)env_off);
+    const uint32_t wb_hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)env_off >> 32));
+    const int64_t wbase = (int64_t)(((uint64_t)wb_hi << 32) | wb_lo);
+    char *isrc = (char *)(out.index + wbase), *idst = (char *)(out.index + out.cap + wbase);
+    char *attr = (char *)(out.attr + wbase);
+    for (int e = L.lane; e < total; e += kWave) {
+        const uint32_t w = s_scr[e];
+        const uint32_t a = w & 0xffu, b = w >> 8;
+        const float2 pa = s_pos[a], pb = s_pos[b];
+        const float dx = pa.x - pb.x, dy = pa.y - pb.y;
+        const uint32_t byte = (uint32_t)e << 2;
+        *(int32_t *)(isrc + byte) = g0 + (int32_t)a;
+        *(int32_t *)(idst + byte) = g0 + (int32_t)b;
+        *(float *)(attr + byte) = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+    }
+}
+
 // CSR offsets of a workgroup's envs: its edge counts (lane k < envs of the
 // block: env first+k) and the sum of the preceding workgroups' edge sums
 // (int4 loads spread over the workgroup's threads). Loads only; the sums are
@@ -547,7 +593,8 @@ __device__ __forceinline__ BlockPrefix block_prefix_loads(const int32_t *block_s
 template <int kN, int kNo, int kG>
 __device__ __forceinline__ void block_emit(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L,
                                            const float2 *s_pos, uint64_t mask, BlockPrefix pre, int *s_red,
-                                           int64_t *edge_ptr, const EdgeSink &out) {
+                                           int64_t *edge_ptr, const EdgeSink &out, uint32_t *s_scr,
+                                           int scr_cap) {
     const int first = blockIdx.x * kWavesPerBlock * s.G;
     const int acc = wave_total(pre.acc);
     if (L.lane == 0) s_red[L.wave] = acc;
@@ -572,7 +619,17 @@ __device__ __forceinline__ void block_emit(const DevParams &p, const Shape<kN, k
 #ifdef GSM_ABL_NO_ROWS   // timing-only ablation (no edges written)
     if (my_cnt < 0)
 #endif
-    emit_rows<kN, kNo, kG>(s, L, s_pos, mask, env_off, out, env_off + my_cnt > out.cap);
+    {
+        if constexpr (kG == 1 && kN > 0 && kN <= 31 && kNo <= 32) {
+            // wave-uniform: the staged path when the env's list fits the scratch
+            // and the outputs (a redirected slot may be smaller than the worst case)
+            if (L.b < p.B && my_cnt <= scr_cap && env_off + my_cnt <= out.cap) {
+                emit_rows_staged<kN, kNo>(L, s_pos, s_scr, mask, env_off, out);
+                return;
+            }
+        }
+        emit_rows<kN, kNo, kG>(s, L, s_pos, mask, env_off, out, env_off + my_cnt > out.cap);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -716,8 +773,10 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     GSM_STAMP(p, wid, 1);
     if constexpr (kLag) {
         // the previous step's edges: its positions (staged above) and row masks
+        // scratch: the staged node-feature / column-pair area (free until the sweep)
         block_emit<kN, kNo, kG>(p, s, L, s_pos, oo, lag_pre, s_lag, p.lag.edge_ptr,
-                                EdgeSink{p.lag.edge_index, p.lag.edge_attr, p.lag.cap});
+                                EdgeSink{p.lag.edge_index, p.lag.edge_attr, p.lag.cap}, (uint32_t *)s_nf,
+                                (p.wave_lds_step - 8 * G * E) / 4);
     }
     GSM_STAMP(p, wid, 2);
 
@@ -983,7 +1042,8 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
     }
     GSM_STAMP(p, wid, 1);
     block_emit<kN, kNo, kG>(p, s, L, s_pos, mask, pre, s_red, p.edge_ptr,
-                            EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity});
+                            EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity}, (uint32_t *)(s_pos + E),
+                            (p.wave_lds_emit - 8 * G * E) / 4);
     GSM_STAMP(p, wid, 4);
     GSM_RSTAMP(p, wid, 9);
 }

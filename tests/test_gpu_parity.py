@@ -185,6 +185,37 @@ def test_boundary_predicates_exact():
     check_outputs(env, ocfg, out)
 
 
+def test_coincident_pairs_one_env_per_wave():
+    """24 agents (one env per wave, the headline sweep): a coincident
+    agent-agent and agent-obstacle pair count as collisions, give no radius
+    edge and no contact force, through set_state (full sweep) and a step."""
+    N, B = 24, 4
+    env, ocfg = _env(n_agents=N, n_envs=B)
+    env.reset(seed=0)
+    E = 3 * N
+    rng = np.random.default_rng(5)
+    gx, gy = np.meshgrid(np.arange(9), np.arange(8))
+    grid = (np.stack([gx.ravel(), gy.ravel()], -1)[:E] * 0.62 - 2.5).astype(np.float32)
+    pos = np.stack([grid + rng.uniform(-0.05, 0.05, grid.shape).astype(np.float32) for _ in range(B)])
+    pos[1, 7] = pos[1, 3]                # agent-agent
+    pos[1, 5] = pos[1, 2 * N + 2]        # agent-obstacle
+    pos[2, 0] = pos[2, 2 * N]            # agent-obstacle, obstacle 0
+    out = env.set_state(dict(pos=torch.from_numpy(pos), vel=torch.zeros(B, N, 2)))
+    torch.cuda.synchronize()
+    check_outputs(env, ocfg, out)
+    check_cost_reward(env, ocfg, out)
+    assert _np(out["cost"])[1, [3, 7, 5]].tolist() == [1.0, 1.0, 1.0]
+    for _ in range(2):
+        out = env.step(torch.zeros(B, N, dtype=torch.int32, device=DEV))
+        torch.cuda.synchronize()
+        assert np.all(np.isfinite(_np(env.t["pos"])))
+        check_outputs(env, ocfg, out)
+        check_cost_reward(env, ocfg, out)
+    p = _np(env.t["pos"])
+    assert np.array_equal(p[1, 7], p[1, 3]) and np.array_equal(p[1, 5], p[1, 2 * N + 2])
+    assert _np(out["cost"])[2, 0] == 1.0
+
+
 # ------------------------------------------------------------- episodes
 @pytest.mark.parametrize("N,B", [(3, 1), (3, 256), (24, 64), (96, 16), (40, 8)])
 def test_episode_rollout_stepwise(N, B):
