@@ -9,11 +9,13 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
 #include "gsm.h"
 #include "gsm_internal.h"
+#include "gsm_philox.h"
 
 struct gsm_handle {
     gsm_config cfg;
@@ -24,6 +26,7 @@ struct gsm_handle {
     // graph capture
     hipStream_t cap_stream = nullptr;
     int32_t *bsum_alt = nullptr;   // second half of the per-workgroup edge-sum double buffer (lagged emission)
+    int32_t *block_order = nullptr;   // ragged mixed: workgroup -> env block, heaviest first
     struct Slot {
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
@@ -51,6 +54,45 @@ int hip_fail(gsm_handle *h, hipError_t e, const char *where) {
 }
 
 int align16(int x) { return (x + 15) & ~15; }
+
+// Ragged mixed batches: the step kernel's workgroups take their env blocks
+// heaviest first, so the long assignment chains (polygon/line envs with many
+// agents) start in the first residency round instead of waiting behind light
+// envs. Cost of an env ~ N_env^2 for polygon/line (assignment path
+// iterations), N_env for navigation; a block costs its heaviest env. The
+// order only schedules: every output is the same under any order (each
+// workgroup writes its own env block's slots). Recomputed when the seed that
+// draws the env shapes changes (a host-to-device copy then; never per step).
+int update_block_order(gsm_handle *h) {
+    const gsm::DevParams &p = h->dp;
+    if (p.path != gsm::kPathRagged || p.scenario != gsm::kScnMixed) return GSM_OK;
+    const int nb = h->sz.n_blocks, per = h->sz.envs_per_block;
+    std::vector<int64_t> key(nb);
+    for (int k = 0; k < nb; ++k) {
+        int64_t c = 0;
+        for (int b = k * per; b < (k + 1) * per && b < p.B; ++b) {
+            const int64_t gid = p.env_base + b;
+            const gsm::Philox4 x = gsm::philox4x32_10(0u, 0u, (uint32_t)gid, gsm::kTagShape, p.seed_lo, p.seed_hi);
+            const int n = p.n_min + (int)(((uint64_t)x.x0 * (uint64_t)(p.N - p.n_min + 1)) >> 32);
+            const int64_t ce = (gid % 3) != gsm::kScnNav ? (int64_t)n * n : n;
+            c = ce > c ? ce : c;
+        }
+        key[k] = c;
+    }
+    std::vector<int32_t> order(nb);
+    for (int k = 0; k < nb; ++k) order[k] = k;
+    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key[a] > key[b]; });
+    hipError_t e = hipSuccess;
+    if (!h->block_order) e = hipMalloc(&h->block_order, (size_t)nb * sizeof(int32_t));
+    if (e != hipSuccess) {
+        h->block_order = nullptr;
+        return hip_fail(h, e, "hipMalloc (block order)");
+    }
+    e = hipMemcpy(h->block_order, order.data(), (size_t)nb * sizeof(int32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) return hip_fail(h, e, "hipMemcpy (block order)");
+    h->dp.block_order = h->block_order;
+    return GSM_OK;
+}
 
 int check_config(const gsm_config *c, std::string *why) {
     if (!c) { *why = "config is NULL"; return GSM_EINVAL; }
@@ -327,6 +369,8 @@ int gsm_bind(gsm_handle *h, const gsm_buffers *b) {
     if (ragged) {
         const hipError_t e = gsm::upload_ragged_tables();
         if (e != hipSuccess) return hip_fail(h, e, "ragged constant tables");
+        const int rc = update_block_order(h);
+        if (rc) return rc;
     }
     if (((uintptr_t)b->pos | (uintptr_t)b->vel | (uintptr_t)b->ep_acc | (uintptr_t)b->ep_last) & 7)
         return fail(h, GSM_EINVAL, "pos/vel/ep_acc/ep_last must be 8-byte aligned");
@@ -362,6 +406,10 @@ int gsm_reset(gsm_handle *h, uint64_t seed, int reseed, const uint8_t *env_mask,
         h->dp.seed_lo = (uint32_t)(seed & 0xFFFFFFFFull);
         h->dp.seed_hi = (uint32_t)(seed >> 32);
         drop_graph(h);   // captured auto-resets would use the old key
+        if (h->bound) {
+            const int rc = update_block_order(h);   // mixed: the env shapes follow the seed
+            if (rc) return rc;
+        }
     }
     return launch(h, GSM_MODE_RESET, nullptr, 0, env_mask, reseed ? 1 : 0, as_stream(stream));
 }
@@ -622,6 +670,7 @@ int gsm_destroy(gsm_handle *h) {
     drop_graph(h);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->bsum_alt) (void)hipFree(h->bsum_alt);
+    if (h->block_order) (void)hipFree(h->block_order);
     delete h;
     return GSM_OK;
 }

@@ -52,6 +52,7 @@ struct DevParams {
     uint64_t *contact_mask;   // [B][N] contact candidates (segmented path)
     int32_t *env_shape;       // [B] ragged: N_env | scenario << 8
     int32_t *assign;          // [B][N] ragged: LSA slot per agent
+    const int32_t *block_order;   // ragged mixed: workgroup -> env block, heaviest first (nullptr: identity)
     int64_t edge_capacity;
     const void *actions;
     const uint8_t *env_mask;

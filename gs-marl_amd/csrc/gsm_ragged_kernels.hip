@@ -79,6 +79,25 @@ __device__ __forceinline__ int max32(int v) {
     v = max(v, dpp_keep<0x142, 0xa>(v));
     return __builtin_amdgcn_readlane(v, 31);
 }
+// DPP source whose unwritten lanes read INT_MAX, the identity of min: the
+// compiler folds each move into its v_min_i32_dpp
+template <int kCtrl, int kRowMask = 0xf>
+__device__ __forceinline__ int dpp_any(int v) {
+    return __builtin_amdgcn_update_dpp(0x7fffffff, v, kCtrl, kRowMask, 0xf, false);
+}
+__device__ __forceinline__ int min32_i(int v) {
+    v = min(v, dpp_any<0xB1>(v));
+    v = min(v, dpp_any<0x4E>(v));
+    v = min(v, dpp_any<0x141>(v));
+    v = min(v, dpp_any<0x140>(v));
+    v = min(v, dpp_any<0x142, 0xa>(v));
+    return __builtin_amdgcn_readlane(v, 31);
+}
+// float -> int with the same order for every non-NaN value
+__device__ __forceinline__ int f32_order_key(float f) {
+    const int b = __float_as_int(f);
+    return b ^ ((b >> 31) & 0x7fffffff);
+}
 __device__ __forceinline__ int first_lane(uint64_t m) { return __builtin_ctzll(m); }
 
 struct RShape {
@@ -142,69 +161,101 @@ __device__ __forceinline__ float2 slot_of(const DevParams &p, const RShape &s, i
 // row k and column k. C[i][j] = |p_i - slot_j| in fp32 (staged in LDS),
 // all dual arithmetic in float64 in scipy's operation order. Returns the
 // lane's column (row `lane`), and its cost in *own.
-__device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, float *own) {
+__device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, float *own, int *iters = nullptr) {
     const bool col = lane < N;
 #ifdef GSM_ABL_NO_LSA   // timing-only ablation: identity assignment
     *own = 0.0f;
     return col ? lane : -1;
 #endif
-    for (int i = 0; i < N; ++i) {
-        const float2 pi = rl_f2(pa, i);
-        if (col) {
+    // column `lane` of C held in registers, C[i][lane] picked by the
+    // wave-uniform row i (s_set_gpr_idx): no LDS round trip in the path loop;
+    // the LDS copy serves the final cost lookup
+    float ccol[kRaggedMaxAgents];
+#pragma unroll
+    for (int i = 0; i < kRaggedMaxAgents; ++i) {
+        float c = 0.0f;
+        if (i < N) {
+            const float2 pi = rl_f2(pa, i);
             const float dx = pi.x - slot.x, dy = pi.y - slot.y;
-            s_cost[i * N + lane] = sqrtf(dx * dx + dy * dy);
+            c = sqrtf(dx * dx + dy * dy);
+            if (col) s_cost[i * N + lane] = c;
         }
+        ccol[i] = c;
     }
     wave_sync();
     const double kInf = __builtin_inf();
     double u = 0.0, v = 0.0;
     int col4row = -1, row4col = -1;
+    const uint64_t colmask = N >= 64 ? ~0ull : ((1ull << N) - 1);
     for (int cur = 0; cur < N; ++cur) {
         double spc = kInf;
         int path = -1;
-        bool SR = false, SC = false;
         int rpos = N - 1 - lane;     // position in scipy's `remaining` list (filled in reverse)
         int nrem = N;
         double minVal = 0.0;
         int i = cur, sink = -1;
+        // Wave-uniform bit sets: columns still in `remaining`, rows visited.
+        // The iteration has no divergent branch; its chain is: dual of row i
+        // and C[i][j] -> reduced cost -> 32-bit minimum key -> (the unique
+        // minimum, else an exact f64 reduction among the near ones) -> the
+        // column's row.
+        uint64_t remm = colmask, srm = 0;
         // a square problem reaches a free column within N scans; the bound
         // only guarantees termination should the invariants ever break
-        for (int guard = 0; sink < 0 && guard < N; ++guard) {
-            if (lane == i) SR = true;
+        for (int guard = 0; guard < N; ++guard) {
+#ifdef GSM_STAMPS   // diagnostic builds: path iterations
+            if (iters) ++*iters;
+#endif
+            srm |= 1ull << i;
             const double ui = rl_d(u, i);
-            const bool rem = col && !SC;
-            if (rem) {
-                const double r = minVal + (double)s_cost[i * N + lane] - ui - v;
-                if (r < spc) {
-                    path = i;
-                    spc = r;
-                }
-            }
+            const bool rem = (remm >> lane) & 1;
+            const double r = minVal + (double)ccol[i] - ui - v;
+            const bool upd = rem && r < spc;
+            path = upd ? i : path;
+            spc = upd ? r : spc;
             // scipy scans `remaining` in order and keeps the first minimum
             // unless a later equal one is unassigned: the last unassigned
-            // minimum in scan order if any, else the first minimum. With
-            // continuous costs the minimum is almost always unique; ties take
-            // one more reduction over key = 64 + pos (unassigned) or 63 - pos
-            // (assigned), larger key winning (keys are distinct).
-            const double m = min32(rem ? spc : kInf);
-            const uint64_t cand = __builtin_amdgcn_ballot_w64(rem && spc == m);
-            if (!cand) break;
-            int jsel = first_lane(cand);
-            if (cand & (cand - 1)) {
-                const int key = (rem && spc == m) ? (row4col == -1 ? 64 + rpos : 63 - rpos) : -1;
-                const int kb = max32(key);
-                jsel = first_lane(__builtin_amdgcn_ballot_w64(key == kb));
+            // minimum in scan order if any, else the first minimum. The
+            // minimum is found over a 32-bit key first (spc rounded to float:
+            // monotone; -0 folded into +0; in integer order) with one DPP
+            // reduction: the lanes whose key equals the smallest key hold
+            // every exact minimum, so a single such lane IS the minimum and
+            // several (near or exact ties) take the f64 reduction among them;
+            // exact ties then take one more reduction over key = 64 + pos
+            // (unassigned) or 63 - pos (assigned), larger key winning.
+            const int key = rem ? f32_order_key((float)spc + 0.0f) : 0x7fffffff;
+            const int kmin = min32_i(key);
+            const uint64_t near = __builtin_amdgcn_ballot_w64(key == kmin) & remm;
+            if (!near) break;
+            int jsel;
+            double m;
+            if (__builtin_expect(!(near & (near - 1)), 1)) {
+                jsel = first_lane(near);
+                m = rl_d(spc, jsel);
+            } else {
+                m = min32((near >> lane) & 1 ? spc : kInf);
+                const uint64_t cand = __builtin_amdgcn_ballot_w64(spc == m) & remm;
+                jsel = first_lane(cand);
+                if (cand & (cand - 1)) {
+                    const int tkey = (cand >> lane) & 1 ? (row4col == -1 ? 64 + rpos : 63 - rpos) : -1;
+                    const int kb = max32(tkey);
+                    jsel = first_lane(__builtin_amdgcn_ballot_w64(tkey == kb));
+                }
             }
             minVal = m;
             const int r4c = __builtin_amdgcn_readlane(row4col, jsel);
             const int at = __builtin_amdgcn_readlane(rpos, jsel);
-            if (lane == jsel) SC = true;
+            remm &= ~(1ull << jsel);
             nrem -= 1;
-            if (rem && lane != jsel && rpos == nrem) rpos = at;   // remaining[index] = remaining[--n]
-            if (r4c < 0) sink = jsel;
-            else i = r4c;
+            rpos = (rem && lane != jsel && rpos == nrem) ? at : rpos;   // remaining[index] = remaining[--n]
+            if (r4c < 0) {
+                sink = jsel;
+                break;
+            }
+            i = r4c;
         }
         if (sink < 0) break;   // unreachable for finite costs
+        const bool SR = (srm >> lane) & 1, SC = ((colmask & ~remm) >> lane) & 1;
         // dual update (before augmenting: col4row is the previous matching)
         const double spc_c = __shfl(spc, col4row < 0 ? 0 : col4row);
         if (lane == cur) u += minVal;
@@ -338,7 +389,13 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
     } else {
         slot = slot_of(p, s, lane, tp);
         float own;
-        sigma = wave_lsa(s.N, lane, cp, slot, s_cost, &own);
+        int nit = 0;
+        GSM_STAMP(p, b, 0);
+        sigma = wave_lsa(s.N, lane, cp, slot, s_cost, &own, &nit);
+        GSM_STAMP(p, b, 1);
+#ifdef GSM_STAMPS
+        if (p.stamps && lane == 0) p.stamps[(int64_t)b * 16 + 2] = (uint64_t)nit;
+#endif
         r = -own;
     }
     float rsum = wave_sum(lane < s.N ? r : 0.0f);
@@ -435,8 +492,10 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
 
 __global__ __launch_bounds__(kBlock) void gsm_step_ragged_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int b = blockIdx.x * kWavesPerBlock + wave;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: env shape, loops and assignment state stay scalar
+    // env block of this workgroup (mixed: heaviest first, gsm_abi.hip update_block_order)
+    const int blk = p.block_order ? p.block_order[blockIdx.x] : (int)blockIdx.x;
+    const int b = blk * kWavesPerBlock + wave;
     int edges = 0;
     if (b < p.B) edges = ragged_env_step(p, b, lane, smem + wave * p.wave_lds_step);
     int *s_bc = (int *)(smem + kWavesPerBlock * p.wave_lds_step);
@@ -445,7 +504,7 @@ __global__ __launch_bounds__(kBlock) void gsm_step_ragged_kernel(DevParams p) {
     if (threadIdx.x == 0) {
         int sum = 0;
         for (int w = 0; w < kWavesPerBlock; ++w) sum += s_bc[w];
-        p.block_edge_sum[blockIdx.x] = sum;
+        p.block_edge_sum[blk] = sum;
     }
 }
 
@@ -523,7 +582,7 @@ __device__ void ragged_env_emit(const DevParams &p, const int b, const int lane,
 
 __global__ __launch_bounds__(kBlock) void gsm_emit_ragged_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     int *s_red = (int *)(smem + kWavesPerBlock * p.wave_lds_emit);
     // exclusive prefix of the step kernel's per-workgroup edge sums
     int acc = 0;
