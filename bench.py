@@ -40,7 +40,7 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def step_kernel_bytes(B, N, No, EL, action_bytes, seg=True):
+def step_kernel_bytes(B, N, No, EL, action_bytes, seg=True, envs_per_block=None):
     """Algorithmic HBM bytes of one step-kernel launch.
 
     Segmented path (M = N + No <= 64): per env, reads pos of every entity,
@@ -58,7 +58,7 @@ def step_kernel_bytes(B, N, No, EL, action_bytes, seg=True):
         reads = 8 * E + 8 * N + action_bytes * N + 16 + 8 * N + 8 * No
         writes = 8 * N + 8 * N + 28 * N + 4 * N + 4 * N + 8 * N + 8 * M + 16 + 1 + 4
         reset = (8 * (E - N) + 28 * (E - N) + 8) / EL
-        per_block = 4 * min(64 // M, 16)
+        per_block = envs_per_block or 4 * min(64 // M, 4)   # gsm_sizes.envs_per_block
     else:
         W, ka = (M + 63) // 64, (N + 63) // 64
         reads = 8 * E + 8 * N + action_bytes * N + 16 + 8 * N * W + 8 * No * (W - ka)
@@ -347,7 +347,7 @@ def main():
             sb, eb = ragged_kernel_bytes(env, EL, 4, edges_now)
             names = ("gsm_step_ragged_kernel", "gsm_emit_ragged_kernel")
         else:
-            sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4, seg)
+            sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4, seg, env.sizes.envs_per_block)
             if lag:
                 sb += lag_extra_bytes(B, N, cfg.n_obstacles, edges_now, seg)
             eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)

@@ -152,8 +152,14 @@ void choose_path(const gsm_config *c, int *path, int *G) {
         *G = 1;
     } else if (M <= gsm::kWave) {
         *path = gsm::kPathSeg;
+        // as many envs per wave as fit (at most kMaxSegEnvsPerWave), but no
+        // fewer waves than one workgroup per CU (256 x 4): a small batch of
+        // small envs is latency-bound, and packing it into fewer waves leaves
+        // CUs idle
         int g = gsm::kWave / M;
-        *G = g > gsm::kMaxSegEnvsPerWave ? gsm::kMaxSegEnvsPerWave : g;
+        g = g > gsm::kMaxSegEnvsPerWave ? gsm::kMaxSegEnvsPerWave : g;
+        const int64_t fill = c->n_envs / 1024;
+        *G = fill < g ? (fill < 1 ? 1 : (int)fill) : g;
     } else {
         *path = gsm::kPathTile;
         *G = 1;

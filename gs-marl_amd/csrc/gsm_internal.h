@@ -16,7 +16,10 @@ constexpr int kTileBlock = GSM_TILE_BLOCK;     // tile path: one workgroup per e
 enum : int32_t { kScnNav = 0, kScnPolygon = 1, kScnLine = 2, kScnMixed = 3 };
 constexpr int kRaggedMaxAgents = 32;                                  // = GSM_RAGGED_MAX_AGENTS
 constexpr int kRaggedTable = kRaggedMaxAgents * (kRaggedMaxAgents + 1) / 2;   // rows n = 1..32
-constexpr int kMaxSegEnvsPerWave = 16;   // keeps a block's envs (4G) within one wave's lanes
+#ifndef GSM_SEG_GMAX   // cap on envs per wave (C2, 3 x 4096: G = 4 runs 6.0 us per step against 6.9 at G = 10)
+#define GSM_SEG_GMAX 4
+#endif
+constexpr int kMaxSegEnvsPerWave = GSM_SEG_GMAX;   // keeps a block's envs (4G) within one wave's lanes
 
 // Everything a launch needs, passed by value (kernarg segment, < 4 KB).
 // fp32 constants are formed on the host exactly as oracle/batch_ref.py:Spec

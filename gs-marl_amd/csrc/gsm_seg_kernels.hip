@@ -1056,7 +1056,7 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
 template <bool LAG>
 static const void *pick_step_seg(const DevParams &p) {
 #define GSM_PICK(n, no)                                                                       \
-    if (p.N == n && p.No == no) {                                                             \
+    if (p.N == n && p.No == no && p.G == envs_per_wave<n, no>()) {                           \
         switch (p.action_fmt) {                                                               \
             case 0: return reinterpret_cast<const void *>(&gsm_step_seg_kernel<n, no, 0, LAG>); \
             case 1: return reinterpret_cast<const void *>(&gsm_step_seg_kernel<n, no, 1, LAG>); \
@@ -1072,7 +1072,8 @@ const void *lag_step_seg_kernel_fn(const DevParams &p) { return pick_step_seg<tr
 
 const void *emit_seg_kernel_fn(const DevParams &p) {
 #define GSM_PICK(n, no) \
-    if (p.N == n && p.No == no) return reinterpret_cast<const void *>(&gsm_emit_seg_kernel<n, no>);
+    if (p.N == n && p.No == no && p.G == envs_per_wave<n, no>()) \
+        return reinterpret_cast<const void *>(&gsm_emit_seg_kernel<n, no>);
     GSM_SEG_SHAPES(GSM_PICK)
 #undef GSM_PICK
     return reinterpret_cast<const void *>(&gsm_emit_seg_kernel<0, 0>);
