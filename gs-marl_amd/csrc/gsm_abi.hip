@@ -227,8 +227,13 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
         // one env per wave: + the staged edge list (emit_rows_staged)
         p->wave_lds_emit = align16(p->G == 1 ? 36 * p->E : 8 * p->G * p->E);
     } else {
-        // tile: whole-workgroup LDS: positions, velocities, new positions, costs, reductions
+        // tile: whole-workgroup LDS: positions, velocities, new positions, costs, reductions;
+        // + the symmetric sweep's column pairs, agent-row words and obstacle-row
+        // agent bits when they fit in 32 KB (gsm_tile_kernels.hip: obs_sweep_sym)
         p->wave_lds_step = align16(8 * p->E + 8 * N + 8 * N + 4 * N + 8 * (gsm::kTileBlock / gsm::kWave));
+        const int sym = 16 * ((N + 1) / 2) + 16 * N * p->W + 8 * No * p->W + 16;
+        p->tile_sym = sym <= 32768;
+        if (p->tile_sym) p->wave_lds_step += sym;
         p->wave_lds_emit = align16(8 * p->E + 4 * (gsm::kTileBlock / gsm::kWave));
     }
     const float L = c->world_half;

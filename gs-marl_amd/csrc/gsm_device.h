@@ -12,6 +12,15 @@ enum { kModeStep = 0, kModeReset = 1, kModeObserve = 2 };
 // still schedules it and resolves its hazards)
 __device__ uint32_t writelane_u32(uint32_t src, uint32_t lane, uint32_t old) __asm("llvm.amdgcn.writelane.i32");
 
+// 2*own + (this lane's bit of `lanes`): one v_addc per column (the compiler
+// builds own |= bit << j from a select and a shift-or)
+__device__ __forceinline__ uint32_t shl1_add_lane(uint32_t own, uint64_t lanes) {
+    uint32_t r;
+    uint64_t co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(own), "s"(lanes));
+    return r;
+}
+
 // Orders LDS traffic between the lanes of one wave: LDS ops of a wave execute
 // in order, so only compiler motion has to be fenced.
 __device__ __forceinline__ void wave_sync() {

@@ -34,6 +34,7 @@ struct DevParams {
     int32_t W;             // uint64 words per mask row (tile path: ceil(M/64))
     int32_t nf_full;       // write every node-feature row (redirected outputs)
     int32_t G;             // envs per wave (segmented path), 1 otherwise
+    int32_t tile_sym;      // tile path: symmetric sweep (its LDS fits), gsm_tile_kernels.hip
     uint32_t seed_lo, seed_hi;
     int64_t env_base;
     int32_t wave_lds_step, wave_lds_emit;      // bytes of LDS per wave

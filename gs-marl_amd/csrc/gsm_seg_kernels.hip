@@ -145,15 +145,6 @@ __device__ __forceinline__ T seg_total(T v, const Lane &L, int M) {
 template <int kN>
 using OwnBits = typename std::conditional<(kN > 0 && kN <= 32), uint32_t, uint64_t>::type;
 
-// 2*own + (this lane's bit of `lanes`): one v_addc per column (the compiler
-// builds own |= bit << j from a select and a shift-or)
-__device__ __forceinline__ uint32_t shl1_add_lane(uint32_t own, uint64_t lanes) {
-    uint32_t r;
-    uint64_t co;
-    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(own), "s"(lanes));
-    return r;
-}
-
 // low 16 bits of a, low 16 bits of b above them (one s_pack_ll_b32_b16)
 __device__ __forceinline__ uint32_t pack_lo16(uint64_t a, uint64_t b) {
     uint32_t r;

@@ -160,6 +160,169 @@ __device__ __forceinline__ int obs_sweep(const DevParams &p, const float2 *s_pos
     return pairs;
 }
 
+// Symmetric sweep (when its LDS fits, p.tile_sym): lanes are ROWS and the
+// loop runs over agent COLUMNS, as on the one-env-per-wave path. A unit is
+// (row chunk c, 8 agent columns j0..j0+7): per column j the wave ballots the
+// rows m of chunk c with rad'(m, j) = d2 <= R^2 and near(m, j) = d2 < cut^2 —
+// by symmetry agent row j's words c of the radius and contact-candidate
+// masks. Each agent pair is evaluated once per (chunk, column) instead of
+// once from each side, on column pairs staged for packed-f32 distances
+// (s_xy: [x_j x_j+1 y_j y_j+1]); obstacle rows collect their agent-column
+// bits with one v_addc per column (a byte per unit), their obstacle-obstacle
+// bits stay cached (keep_oo) or are recomputed on a new layout. Agent rows
+// then walk their near bits: collisions (d2 < dmin^2 implies d2 < cut^2) and
+// the stored candidates without the self and coincident pairs; a coincident
+// pair anywhere in the env (never seen in practice) re-derives every row with
+// the exact 0 < d2 <= R^2. Same outputs as obs_sweep.
+struct TileSymLds {
+    float *xy;        // [ceil(N/2)][4]
+    uint64_t *arow;   // [N][2W]: radius words, then near words of agent rows
+    uint64_t *own;    // [No][W]: agent-column bits of obstacle rows
+    int *flag;        // coincident pair seen
+};
+
+__device__ __forceinline__ uint64_t agent_bits_of_word(int N, int k) {   // agent columns of mask word k
+    const int lo = 64 * k;
+    return N <= lo ? 0ull : (N >= lo + 64 ? ~0ull : ((1ull << (N - lo)) - 1ull));
+}
+
+__device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s_pos, const TileSymLds &S,
+                                             int *s_cost, int64_t eb, bool keep_oo) {
+    typedef float f32x2 __attribute__((ext_vector_type(2)));
+    const int N = p.N, M = p.M, W = p.W, No = p.No;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int NB8 = (N + 7) >> 3, NP = (N + 1) >> 1;
+    const float2 far = make_float2(1.0e18f, 1.0e18f);       // d2 ~ 1e36: every predicate false
+    for (int j = tid; j < 2 * NP; j += kTileBlock) {
+        const float2 a = j < N ? s_pos[j] : far;
+        const int at = (j >> 1) * 4 + (j & 1);
+        S.xy[at] = a.x;
+        S.xy[at + 2] = a.y;
+    }
+    for (int k = tid; k < No * W; k += kTileBlock) S.own[k] = 0ull;
+    if (tid == 0) *S.flag = 0;
+    __syncthreads();
+    const float R2 = p.R2;
+    const int U = W * NB8;
+    for (int u = wave; u < U; u += kTileWaves) {
+        const int c = u / NB8, jb = u - c * NB8;
+        const int m = 64 * c + lane;
+        const bool live = m < M, obst = live && m >= N;
+        const float2 pm = live ? s_pos[collider_entity(m, N)] : far;
+        const float cut2 = obst ? p.cut2_ao : p.cut2_aa;
+        const f32x2 px = {pm.x, pm.x}, py = {pm.y, pm.y};
+        const int j0 = 8 * jb, nc = min(8, N - j0);
+        const float4 *xy4 = (const float4 *)S.xy + (j0 >> 1);
+        uint32_t rlo = 0, rhi = 0, nlo = 0, nhi = 0, own = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (2 * q >= nc) break;
+            const float4 Q = xy4[q];
+            const f32x2 dx = px - (f32x2){Q.x, Q.y}, dy = py - (f32x2){Q.z, Q.w};
+            const f32x2 d2 = dx * dx + dy * dy;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int k = 2 * q + h;
+                if (k >= nc) break;
+                const float dd = h ? d2.y : d2.x;
+                const uint64_t br = __builtin_amdgcn_ballot_w64(dd <= R2);
+                const uint64_t bn = __builtin_amdgcn_ballot_w64(dd < cut2);
+                own = shl1_add_lane(own, br);
+                rlo = writelane_u32((uint32_t)br, (uint32_t)k, rlo);
+                rhi = writelane_u32((uint32_t)(br >> 32), (uint32_t)k, rhi);
+                nlo = writelane_u32((uint32_t)bn, (uint32_t)k, nlo);
+                nhi = writelane_u32((uint32_t)(bn >> 32), (uint32_t)k, nhi);
+            }
+        }
+        if (lane < nc) {
+            uint64_t *ar = S.arow + (int64_t)(j0 + lane) * 2 * W;
+            ar[c] = ((uint64_t)rhi << 32) | rlo;
+            ar[W + c] = ((uint64_t)nhi << 32) | nlo;
+        }
+        // obstacle row m, agent columns j0.. j0+nc-1: byte jb of its words
+        if (obst) ((uint8_t *)(S.own + (int64_t)(m - N) * W))[jb] = (uint8_t)(__builtin_bitreverse32(own) >> (32 - nc));
+    }
+    __syncthreads();
+    uint64_t *const rmask = p.row_mask + eb * M * W;
+    uint64_t *const cmask = p.contact_mask + eb * N * W;
+    int pairs = 0, coinc = 0;
+    for (int r = tid; r < M; r += kTileBlock) {
+        const float2 a = s_pos[collider_entity(r, N)];
+        if (r < N) {
+            const uint64_t *ar = S.arow + (int64_t)r * 2 * W;
+            int cnt = 0;
+            for (int k = 0; k < W; ++k) {
+                const uint64_t self = k == (r >> 6) ? 1ull << (r & 63) : 0ull;
+                const uint64_t rad = ar[k] & ~self;
+                uint64_t near = ar[W + k] & ~self, cand = near;
+                while (near) {
+                    const int b = __builtin_ctzll(near);
+                    near &= near - 1;
+                    const int ci = 64 * k + b;
+                    const float2 q = s_pos[collider_entity(ci, N)];
+                    const float dx = a.x - q.x, dy = a.y - q.y;
+                    const float d2 = dx * dx + dy * dy;
+                    cnt += d2 < (ci < N ? p.dmin2_aa : p.dmin2_ao) ? 1 : 0;
+                    if (d2 == 0.0f) {
+                        cand &= ~(1ull << b);
+                        coinc = 1;
+                    }
+                }
+                rmask[(int64_t)r * W + k] = rad;
+                cmask[(int64_t)r * W + k] = cand;
+                pairs += __popcll(rad);
+            }
+            s_cost[r] = cnt;
+        } else {
+            const uint64_t *ow = S.own + (int64_t)(r - N) * W;
+            for (int k = 0; k < W; ++k) {
+                const uint64_t am = agent_bits_of_word(N, k);
+                uint64_t oo = 0;
+                if (keep_oo) {
+                    oo = rmask[(int64_t)r * W + k] & ~am;   // obstacle-obstacle bits: static in an episode
+                } else {
+                    const int c1 = min(64 * k + 64, M);
+                    for (int ci = max(64 * k, N); ci < c1; ++ci) {
+                        const float2 q = s_pos[collider_entity(ci, N)];
+                        const float dx = a.x - q.x, dy = a.y - q.y;
+                        const float d2 = dx * dx + dy * dy;
+                        if (d2 > 0.0f && d2 <= R2) oo |= 1ull << (ci - 64 * k);
+                    }
+                }
+                const uint64_t w = (ow[k] & am) | oo;
+                if (am || !keep_oo) rmask[(int64_t)r * W + k] = w;
+                pairs += __popcll(w);
+            }
+        }
+    }
+    if (coinc) *S.flag = 1;
+    __syncthreads();
+    if (*S.flag) {
+        // exact rows: rad' also held the coincident pairs (agent columns of
+        // every row, obstacle columns of agent rows; obstacle-obstacle bits
+        // are exact already)
+        pairs = 0;
+        for (int r = tid; r < M; r += kTileBlock) {
+            const float2 a = s_pos[collider_entity(r, N)];
+            for (int k = 0; k < W; ++k) {
+                const uint64_t am = agent_bits_of_word(N, k);
+                uint64_t w = r < N ? 0ull : rmask[(int64_t)r * W + k] & ~am;
+                const int c1 = min(64 * k + 64, r < N ? M : N);
+                for (int ci = 64 * k; ci < c1; ++ci) {
+                    const float2 q = s_pos[collider_entity(ci, N)];
+                    const float dx = a.x - q.x, dy = a.y - q.y;
+                    const float d2 = dx * dx + dy * dy;
+                    if (d2 > 0.0f && d2 <= R2) w |= 1ull << (ci - 64 * k);
+                }
+                rmask[(int64_t)r * W + k] = w;
+                pairs += __popcll(w);
+            }
+        }
+    }
+    return pairs;
+}
+
 __device__ __forceinline__ int obs_sweep_any(const DevParams &p, const float2 *s_pos, int *s_cost, int64_t eb,
                                              bool keep_oo) {
     switch (p.W) {
@@ -266,6 +429,18 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
     int *s_cost = (int *)(s_np + N);          // [N]
     int *s_ired = s_cost + N;                 // [kTileWaves]
     float *s_fred = (float *)(s_ired + kTileWaves);
+    // symmetric sweep scratch (p.tile_sym), 16-byte aligned after the above
+    TileSymLds sym;
+    {
+        unsigned char *q = smem + ((8 * E + 8 * N + 8 * N + 4 * N + 8 * kTileWaves + 15) & ~15);
+        sym.xy = (float *)q;
+        q += 16 * ((N + 1) / 2);
+        sym.arow = (uint64_t *)q;
+        q += 16 * N * W;
+        sym.own = (uint64_t *)q;
+        q += 8 * p.No * W;
+        sym.flag = (int *)q;
+    }
     const int64_t eb = b;
 
     // Issue every global read of the step up front (positions, velocities,
@@ -356,7 +531,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
 
     // observation sweep of the post-step state: masks, collision counts, pairs
 #ifndef GSM_ABL_NO_SWEEP
-    int pairs = obs_sweep_any(p, s_pos, s_cost, eb, p.mode == kModeStep && !relaid);
+    int pairs = p.tile_sym ? obs_sweep_sym(p, s_pos, sym, s_cost, eb, p.mode == kModeStep && !relaid)
+                           : obs_sweep_any(p, s_pos, s_cost, eb, p.mode == kModeStep && !relaid);
 #else
     int pairs = 0;
     for (int i = tid; i < N; i += kTileBlock) s_cost[i] = 0;
@@ -387,7 +563,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
         if (done && p.auto_reset) {
             if (tid == 0) p.ep_last[b] = acc;
             relayout();
-            pairs = obs_sweep_any(p, s_pos, s_cost, eb, false);
+            pairs = p.tile_sym ? obs_sweep_sym(p, s_pos, sym, s_cost, eb, false)
+                               : obs_sweep_any(p, s_pos, s_cost, eb, false);
         }
     }
     pairs = tile_sum(pairs, s_ired);
