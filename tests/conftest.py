@@ -31,6 +31,28 @@ def ocfg_factory():
     return make
 
 
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    """Largest position/velocity error seen per test against the fp64 oracle
+    (bar: 1e-6 absolute, tests/parity_tol.py)."""
+    try:
+        from parity_tol import MAX_ERR
+    except ImportError:
+        return
+    if not MAX_ERR:
+        return
+    tr = terminalreporter
+    tr.section("state parity: max |got - fp64 oracle| (bar 1e-6)")
+    for (test, what), err in sorted(MAX_ERR.items()):
+        tr.write_line(f"{err:.3e}  {what:<4} {test}")
+    tr.write_line(f"{max(MAX_ERR.values()):.3e}  overall max")
+    import json
+    import os
+    out = os.environ.get("GSM_MAXERR_JSON")
+    if out:
+        with open(out, "w") as f:
+            json.dump({f"{t}::{w}": e for (t, w), e in sorted(MAX_ERR.items())}, f, indent=1)
+
+
 def pytest_collection_modifyitems(config, items):
     """GPU tests skip (not fail) on a machine without a GPU, unless
     GSM_REQUIRE_GPU=1 demands one (the GPU box runs them with -m gpu)."""

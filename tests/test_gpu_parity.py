@@ -1,8 +1,9 @@
 """HIP step path vs the CPU oracle, through the C ABI (libgsm.so).
 
-Tolerances (north_star): positions/velocities within 1e-6 of the fp64 oracle
-stepped from the *identical* fp32 state (a relative 4-ulp term is added for
-|x| > 8 where one fp32 ulp is ~1e-6); collision-cost counts, edge_ptr and
+Tolerances (north_star): positions/velocities within 1e-6 (absolute) of the
+fp64 oracle stepped from the *identical* fp32 state (tests/parity_tol.py: a
+4-ulp term only where |x| >= 8, where one fp32 ulp is ~1e-6; the largest error
+seen per test is printed at the end of the run); collision-cost counts, edge_ptr and
 edge_index bit-exact vs the fp32-mode oracle evaluated on the kernel's own
 fp32 positions; node features bit-exact; rewards and edge distances within
 2 fp32 ulp.
@@ -12,6 +13,7 @@ import pytest
 import torch
 
 from oracle import batch_ref as br
+from parity_tol import check_state
 
 pytestmark = pytest.mark.gpu
 
@@ -35,14 +37,8 @@ def _np(t):
     return t.detach().cpu().numpy()
 
 
-def _tol(ref):
-    return 1e-6 + 4 * np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64)
-
-
 def assert_state_close(got, ref, what):
-    err = np.abs(got.astype(np.float64) - ref)
-    bad = err > _tol(ref)
-    assert not bad.any(), f"{what}: max err {err.max():.3e} at {np.argwhere(bad)[:5].tolist()}"
+    check_state(got, ref, what)
 
 
 def check_outputs(env, ocfg, out):
@@ -110,9 +106,12 @@ def _inject_random(env, ocfg, L, seed, vel_scale=1.0):
 
 @pytest.mark.parametrize("N,No,B,L", [(3, 3, 64, 0.35), (24, 24, 256, 1.2), (24, 24, 256, 2.83), (5, 2, 37, 0.5), (32, 32, 9, 1.6), (24, 24, 8, 0.3), (8, 8, 16, 0.2),
                                       (96, 96, 16, 3.0), (64, 0, 8, 1.0), (65, 7, 8, 1.5), (1, 0, 4, 1.0),
-                                      (600, 10, 2, 8.0), (40, 40, 8, 0.9)])
+                                      (600, 10, 2, 8.0), (40, 40, 8, 0.9), (3, 3, 4096, 1.0),
+                                      (3, 3, 4096, 0.3), (24, 24, 8192, 2.83)])
 def test_one_step_physics_parity(N, No, B, L):
     env, ocfg = _env(n_agents=N, n_obstacles=No, n_envs=B, episode_length=1000)
+    if (N, No, B) == (3, 3, 4096):   # C2: the specialised <3,3> kernels, 4 envs per wave
+        assert env.sizes.envs_per_block == 16
     env.reset(seed=0)
     pos, vel = _inject_random(env, ocfg, L, seed=N + B)
     rng = np.random.default_rng(5)
@@ -291,7 +290,7 @@ def test_graph_replay_equals_eager_and_deterministic():
 
 
 @pytest.mark.parametrize("N,B,T", [(24, 256, 40), (24, 257, 7), (3, 4000, 1), (3, 123, 2), (5, 37, 9), (7, 64, 6),
-                                   (70, 9, 3), (96, 17, 6)])
+                                   (70, 9, 3), (96, 17, 6), (3, 4096, 7), (3, 4100, 6)])
 def test_lagged_chain_equals_eager(N, B, T):
     """Segmented graphs emit step j's edges from step j+1's kernel (lagged
     emission): the chain must leave every state and output buffer exactly as
@@ -299,6 +298,8 @@ def test_lagged_chain_equals_eager(N, B, T):
     lengths, partial workgroups and auto-resets (episode length 5). Tile
     shapes (M > 64) run the two-kernel chain under both names."""
     env, ocfg = _env(n_agents=N, n_envs=B, episode_length=5)
+    if N == 3 and B >= 4096:   # C2's specialised <3,3> kernels (4 envs per wave)
+        assert env.sizes.envs_per_block == 16
     acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
     keys = ("pos", "vel", "step_count", "episode", "node_feat", "reward", "cost", "done", "edge_count",
             "edge_ptr", "ep_acc", "ep_last", "row_mask", "contact_mask")

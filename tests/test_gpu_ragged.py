@@ -14,6 +14,7 @@ import torch
 from scipy.optimize import linear_sum_assignment as scipy_lsa
 
 from oracle import ragged_ref as rr
+from parity_tol import check_state
 
 pytestmark = pytest.mark.gpu
 
@@ -40,8 +41,6 @@ def _ostate(env, rcfg):
                 seed=int(rcfg.seed))
 
 
-def _tol(ref):
-    return 1e-6 + 4 * np.spacing(np.abs(ref).astype(np.float32)).astype(np.float64)
 
 
 def check_observation(env, rcfg, out):
@@ -104,8 +103,8 @@ def test_step_parity(scenario, N, nmin, B, fmt):
         torch.cuda.synchronize()
         st64, _ = rr.step(rcfg, prev, _np(a), 1 if fmt == "index" else 0, np.float64)
         got_p, got_v = _np(env.t["pos"]).astype(np.float64), _np(env.t["vel"]).astype(np.float64)
-        assert np.all(np.abs(got_p - st64["pos"]) <= _tol(st64["pos"])), "pos"
-        assert np.all(np.abs(got_v - st64["vel"]) <= _tol(st64["vel"])), "vel"
+        check_state(got_p, st64["pos"], "pos")
+        check_state(got_v, st64["vel"], "vel")
         check_observation(env, rcfg, out)
         check_reward_cost(env, rcfg, out)
     env.close()
@@ -129,7 +128,7 @@ def test_rollout_with_auto_reset(shared):
         assert np.array_equal(_np(env.t["episode"]), st64["episode"])
         assert np.array_equal(_np(env.t["step_count"]), st64["step"])
         got_p = _np(env.t["pos"]).astype(np.float64)
-        assert np.all(np.abs(got_p - st64["pos"]) <= _tol(st64["pos"])), ("pos", t)
+        check_state(got_p, st64["pos"], f"pos t={t}")
         check_observation(env, rcfg, out)
         live = np.nonzero(done == 0)[0]
         check_reward_cost(env, rcfg, out, envs=live)
