@@ -191,7 +191,7 @@ def cpu_baseline(cfg, seconds, cores):
             "oracle/ragged_ref.py step over a 30-env mixed sample per process (per-env NumPy, fp64, "
             "assignment via oracle/lsa_ref.py)")
     return dict(value=total / wall, unit="agent-steps/s", cores=cores, kind="port",
-                single_core_value=single,
+                single_core_value=single, cpu_model=cpu_model(),
                 sample=f"{cores} host processes x {seconds:.0f} s of {what}; the reference's own CPU path is "
                        f"absent (readme.md:1)")
 
@@ -206,22 +206,57 @@ def host_cores():
     return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
 
 
-def pmc_traffic(key):
-    """HBM bytes per step-kernel launch from the committed rocprofv3 PMC
-    summary (profiles/pmc_traffic.json, written by tools/pmc_traffic.py)."""
-    p = ROOT / "profiles" / "pmc_traffic.json"
-    if not p.exists():
-        return None
+def kernel_src_hash():
+    """Hash of the kernel sources (gs-marl_amd/csrc/*.hip, *.h): PMC figures
+    are injected into a bench line only when they were collected on exactly
+    these sources (tools/pmc_traffic.py records the hash)."""
+    import hashlib
+    h = hashlib.sha256()
+    for p in sorted((ROOT / "gs-marl_amd" / "csrc").iterdir()):
+        if p.suffix in (".hip", ".h"):
+            h.update(p.name.encode())
+            h.update(p.read_bytes())
+    return h.hexdigest()[:16]
+
+
+PMC_FILE = ROOT / "profiles" / "pmc_kernels.json"
+VALU_ISSUE_CYCLES = 4   # per wave64 VALU instruction and SIMD, measured (DESIGN.md §5)
+N_SIMDS = 1024          # 256 CUs x 4 SIMDs
+CLOCK_GHZ = 2.4         # MI355X max engine clock (MI355X_MICROARCH.md)
+
+
+def pmc_entry(key):
+    """(entry, note) for kernel `key` from profiles/pmc_kernels.json: HBM
+    bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) and
+    VALU/SALU instructions per launch. None when absent or collected on other
+    kernel sources than the ones built here (stale figures are never used)."""
+    if not PMC_FILE.exists():
+        return None, "no profiles/pmc_kernels.json"
     try:
-        d = json.loads(p.read_text())
-        return d.get(key, {}).get("hbm_bytes_per_launch")
-    except Exception:
-        return None
+        d = json.loads(PMC_FILE.read_text())
+    except Exception as e:   # a broken file must not break the bench line
+        return None, f"unreadable pmc file: {e}"
+    if d.get("src_hash") != kernel_src_hash():
+        return None, "stale: profiles/pmc_kernels.json was collected on other kernel sources"
+    e = d.get("entries", {}).get(key)
+    return (e, "ok") if e else (None, f"no PMC entry for {key}")
 
 
-def main():
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks); without torchrun bench.py spawns one process per GPU itself")
     ap.add_argument("--steps", type=int, default=300)
     ap.add_argument("--warmup", type=int, default=50)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="h",
@@ -234,27 +269,123 @@ def main():
     ap.add_argument("--cpu-cores", type=int, default=0, help="host processes for the CPU baseline (0: all, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the roofline timing (null)")
+    ap.add_argument("--no-align", action="store_true",
+                    help="do not advance (untimed) so that the timed region contains an episode boundary")
     ap.add_argument("--eager", action="store_true", help="launch steps eagerly instead of HIP graphs")
     ap.add_argument("--unfused", action="store_true",
                     help="two launches per step in the graphs (no lagged emission)")
-    args = ap.parse_args()
+    # launcher self-test only (tests/test_bench_launcher.py): a CPU stand-in env
+    # module and gloo; the line it prints is marked as not a measurement
+    ap.add_argument("--selftest-env", default=None, help=argparse.SUPPRESS)
+    return ap.parse_args(argv)
 
+
+def align_steps(warmup, steps, EL):
+    """Untimed steps after warmup so that the timed region [P, P+K) holds an
+    episode boundary (every env auto-resets when its step count reaches EL,
+    and all envs start together): P = EL - ceil(K/2) (mod EL)."""
+    return (EL - (steps + 1) // 2 - warmup) % EL
+
+
+def boundaries_in(p, k, EL):
+    """Episode boundaries (auto-resets) inside steps p+1 .. p+k."""
+    return (p + k) // EL - p // EL
+
+
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _spawned_rank(argv, rank, world, port):
+    """Entry of one spawned rank (a fresh interpreter: nothing touched the GPU
+    in it yet)."""
+    os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    run_rank(parse_args(argv))
+
+
+def launch_ranks(args, argv):
+    """`bench.py --gpus N` without torchrun: one spawned process per GPU (the
+    parent never initialises the GPU — torch.cuda.device_count() does not on
+    this image), each joining an RCCL process group; fails (non-zero) when
+    fewer than N GPUs are visible or any rank fails, never falls back to fewer
+    ranks."""
+    import multiprocessing as mp
+    n = args.gpus
+    if args.selftest_env is None:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            log(f"error: --gpus {n} but only {have} GPU(s) visible")
+            return 3
+    port = free_port()
+    ctx = mp.get_context("spawn")
+    procs = [ctx.Process(target=_spawned_rank, args=(argv, r, n, port)) for r in range(n)]
+    for p in procs:
+        p.start()
+    rc = 0
+    for p in procs:
+        p.join()
+        if p.exitcode != 0:
+            log(f"error: rank {procs.index(p)} exited with {p.exitcode}")
+            rc = rc or 1
+            for q in procs:   # a failed rank leaves the others blocked in a collective
+                if q.is_alive():
+                    q.terminate()
+    return rc
+
+
+def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
+    args = parse_args(argv)
+    ws = os.environ.get("WORLD_SIZE")
+    if ws is None:
+        if args.gpus > 1:
+            return launch_ranks(args, argv)
+        return run_rank(args)
+    if int(ws) != args.gpus:
+        log(f"error: WORLD_SIZE={ws} but --gpus={args.gpus}")
+        return 2
+    return run_rank(args)
+
+
+def run_rank(args):
     import torch
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        log(f"note: WORLD_SIZE={world} but --gpus={args.gpus}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    stub = args.selftest_env is not None
+    if stub:
+        import importlib
+        dev = torch.device("cpu")
+        make_env = importlib.import_module(args.selftest_env).make_env
+
+        def sync():
+            pass
+    else:
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+
+        def make_env(cfg, device):
+            from gsmarl_amd import GpuBatchEnv
+            return GpuBatchEnv(cfg, device)
+
+        def sync():
+            torch.cuda.synchronize(dev)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        if stub:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:   # RCCL over xGMI
+            dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
-    from gsmarl_amd import EnvConfig, GpuBatchEnv
-    from gsmarl_amd.distributed import all_reduce_metrics, max_over_ranks, shard_config
+    from gsmarl_amd import EnvConfig
+    from gsmarl_amd.distributed import all_reduce_metrics, shard_config
 
     spec = dict(CONFIGS[args.config])
     cfg_name = spec.pop("desc")
@@ -264,7 +395,7 @@ def main():
         spec["n_envs"] = args.n_envs
     N, B = spec["n_agents"], spec["n_envs"]
     cfg = shard_config(EnvConfig(seed=1234, **spec), rank, world)
-    env = GpuBatchEnv(cfg, dev)
+    env = make_env(cfg, dev)
     EL = cfg.episode_length
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
@@ -272,48 +403,63 @@ def main():
     env.reset(seed=cfg.seed, sync_edges=False)
 
     K, W = args.steps, args.warmup
+    A = 0 if args.no_align else align_steps(W, K, EL)
     chunk = min(K, EL)
     n_chunks, rem = divmod(K, chunk)
     gk = "unfused" if args.unfused else "both"
     if not args.eager:
         if W > 0:
             env.capture(actions, W, timing=False, slot=2, kernels=gk)
+        if A > 0:   # slot 3 is re-captured later by the roofline timing
+            env.capture(actions, A, timing=False, slot=3, kernels=gk)
         env.capture(actions, chunk, timing=False, slot=0, kernels=gk)
         if rem:
             env.capture(actions, rem, timing=False, slot=1, kernels=gk)
-    # warmup
-    if W > 0:
-        if args.eager:
-            for t in range(W):
-                env.step(actions[t % EL], sync_edges=False)
-        else:
-            env.replay(2)
-    torch.cuda.synchronize()
-    metrics = torch.zeros(3, dtype=torch.float64, device=dev)
 
-    def run_chunk(n, slot):
+    def run_steps(n, slot):
         if args.eager:
             for t in range(n):
                 env.step(actions[t % EL], sync_edges=False)
         else:
             env.replay(slot)
 
+    # warmup, then the untimed alignment so the timed region holds an auto-reset
+    if W > 0:
+        run_steps(W, 2)
+    if A > 0:
+        run_steps(A, 3)
+    sync()
+    metrics = torch.zeros(3, dtype=torch.float64, device=dev)
+
     if world > 1:
         dist.barrier()
-    torch.cuda.synchronize()
+    sync()
     t0 = time.perf_counter()
     for _ in range(n_chunks):
-        run_chunk(chunk, 0)
+        run_steps(chunk, 0)
         if world > 1:   # the only collective: per-episode metrics (RCCL/xGMI)
             metrics.copy_(env.episode_metrics())
             all_reduce_metrics(metrics)
     if rem:
-        run_chunk(rem, 1)
-    torch.cuda.synchronize()
+        run_steps(rem, 1)
+    sync()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    elapsed = max_over_ranks(elapsed, device=dev) if world > 1 else elapsed
+
+    # every rank's timed region; value uses the slowest (max over ranks)
+    per_rank = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        gathered = [torch.zeros_like(per_rank) for _ in range(world)]
+        dist.all_gather(gathered, per_rank)
+        times = [float(g.item()) for g in gathered]
+    else:
+        times = [elapsed]
+    elapsed = max(times)
+    # final episode metrics over all ranks (the same RCCL all-reduce)
+    metrics.copy_(env.episode_metrics())
+    all_reduce_metrics(metrics)
+    ep_rew, ep_cost, episodes = (float(x) for x in metrics.cpu())
 
     total_edges = int(env.t["edge_ptr"][B].item())
     seg_cfg = (N + cfg.n_obstacles) <= 64 and not cfg.ragged
@@ -330,65 +476,40 @@ def main():
     # kernel alone, after the timed region. Event nodes between kernels would
     # add their own packet time to every launch.
     roofline = None
-    if not args.no_kernel_timing and not args.eager:
-        L = args.kernel_launches
-        seg = (N + cfg.n_obstacles) <= 64 and not cfg.ragged
-        lag = seg and not args.unfused
-        env.capture(actions, L, slot=3, kernels="lag" if lag else "step", time_ends=True)
-        env.replay(3)
-        torch.cuda.synchronize()
-        step_ms = env.graph_kernel_ms(3)[0]
-        env.capture(None, L, slot=3, kernels="emit", time_ends=True)
-        env.replay(3)
-        torch.cuda.synchronize()
-        emit_ms = env.graph_kernel_ms(3)[1]
-        edges_now = int(env.t["edge_ptr"][B].item())
-        if cfg.ragged:
-            sb, eb = ragged_kernel_bytes(env, EL, 4, edges_now)
-            names = ("gsm_step_ragged_kernel", "gsm_emit_ragged_kernel")
-        else:
-            sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4, seg, env.sizes.envs_per_block)
-            if lag:
-                sb += lag_extra_bytes(B, N, cfg.n_obstacles, edges_now, seg)
-            eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)
-            fam = "seg" if seg else "tile"
-            names = (f"gsm_step_{fam}_kernel" + ("<lagged emission>" if lag else ""), f"gsm_emit_{fam}_kernel")
-        kern = {"step": dict(kernel=names[0], ms=step_ms, bytes=sb, gbs=sb / (step_ms * 1e-3) / 1e9),
-                "emit": dict(kernel=names[1], ms=emit_ms, bytes=eb, gbs=eb / (emit_ms * 1e-3) / 1e9)}
-        # a lagged chain runs the emit kernel once per graph, the step kernel every step
-        dom = "step" if (lag or step_ms >= emit_ms) else "emit"
-        k = kern[dom]
-        other = kern["emit" if dom == "step" else "step"]
-        roofline = dict(kernel=k["kernel"], bound="hbm", achieved=round(k["gbs"], 1), peak=HBM_PEAK_GBS,
-                        unit="GB/s", frac=round(k["gbs"] / HBM_PEAK_GBS, 4),
-                        traffic=pmc_traffic(f"{'lag' if (lag and dom == 'step') else dom}:{cfg.scenario}:N{N}:B{B}"),
-                        algorithmic_bytes_per_launch=int(k["bytes"]), mean_launch_us=round(k["ms"] * 1e3, 3),
-                        timing=f"HIP events around {L} back-to-back graph launches of the kernel",
-                        other_kernel=dict(kernel=other["kernel"], achieved=round(other["gbs"], 1),
-                                          algorithmic_bytes_per_launch=int(other["bytes"]),
-                                          mean_launch_us=round(other["ms"] * 1e3, 3)))
-        log(f"kernels: {json.dumps(kern)}")
+    if not args.no_kernel_timing and not args.eager and not stub:
+        roofline = kernel_roofline(env, cfg, actions, args, N, B, EL)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and not stub:
         cpu = cpu_baseline(cfg, args.cpu_seconds, args.cpu_cores or host_cores())
 
     if rank == 0:
+        P = W + A
+        gb = world * B
         line = {
             "metric": METRIC, "value": round(value, 1), "unit": "agent-steps/s", "n_gpus": world,
             "steps": K, "warmup": W, "ms_per_step": round(ms_per_step, 5), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic: Philox4x32-10 layouts, uniform random discrete actions pre-generated on device",
+            "data": ("SELFTEST STUB (CPU stand-in env, not a measurement)" if stub else
+                     "synthetic: Philox4x32-10 layouts, uniform random discrete actions pre-generated on device"),
             "config": {"workload": (f"cooperative_navigation {N} agents x {B} envs per GPU "
                                     f"({N} goals, {cfg.n_obstacles} obstacles; {cfg_name})") if not cfg.ragged
                        else f"{cfg.scenario} up to {N} agents x {B} envs per GPU ({cfg_name})",
-                       "scenario": cfg.scenario, "n_agents": N, "n_envs_per_gpu": B, "global_envs": world * B,
+                       "scenario": cfg.scenario, "n_agents": N, "n_envs_per_gpu": B, "global_envs": gb,
                        "agents_per_step": agents,
                        "episode_length": EL, "mean_edges_per_env": round(total_edges / B, 2),
                        "parallelism": f"env-sharded x{world} (no data-path collective)",
                        "launch": "eager" if args.eager else ("hip-graph per 100-step episode" + (
                            ", lagged emission (one launch per step)" if (seg_cfg and not args.unfused)
                            else ", step + emit launch per step"))},
+            "timed_region": {"untimed_steps_before": P, "align_steps": A,
+                             "episode_boundaries": boundaries_in(P, K, EL),
+                             "rank_ms_per_step_max": round(max(times) / K * 1e3, 5),
+                             "rank_ms_per_step_min": round(min(times) / K * 1e3, 5)},
+            "episode_metrics": {"envs": gb, "finished_episodes": int(episodes),
+                                "mean_last_episode_reward": round(ep_rew / gb, 4),
+                                "mean_last_episode_cost": round(ep_cost / gb, 4),
+                                "reduce": "all_reduce(SUM) over ranks" if world > 1 else "single rank"},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
@@ -396,7 +517,65 @@ def main():
     env.close()
     if world > 1:
         dist.destroy_process_group()
+    return 0
+
+
+def kernel_roofline(env, cfg, actions, args, N, B, EL):
+    import torch
+    L = args.kernel_launches
+    seg = (N + cfg.n_obstacles) <= 64 and not cfg.ragged
+    lag = seg and not args.unfused
+    env.capture(actions, L, slot=3, kernels="lag" if lag else "step", time_ends=True)
+    env.replay(3)
+    torch.cuda.synchronize()
+    step_ms = env.graph_kernel_ms(3)[0]
+    env.capture(None, L, slot=3, kernels="emit", time_ends=True)
+    env.replay(3)
+    torch.cuda.synchronize()
+    emit_ms = env.graph_kernel_ms(3)[1]
+    edges_now = int(env.t["edge_ptr"][B].item())
+    if cfg.ragged:
+        sb, eb = ragged_kernel_bytes(env, EL, 4, edges_now)
+        names = ("gsm_step_ragged_kernel", "gsm_emit_ragged_kernel")
+    else:
+        sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4, seg, env.sizes.envs_per_block)
+        if lag:
+            sb += lag_extra_bytes(B, N, cfg.n_obstacles, edges_now, seg)
+        eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)
+        fam = "seg" if seg else "tile"
+        names = (f"gsm_step_{fam}_kernel" + ("<lagged emission>" if lag else ""), f"gsm_emit_{fam}_kernel")
+    kern = {"step": dict(kernel=names[0], ms=step_ms, bytes=sb, gbs=sb / (step_ms * 1e-3) / 1e9),
+            "emit": dict(kernel=names[1], ms=emit_ms, bytes=eb, gbs=eb / (emit_ms * 1e-3) / 1e9)}
+    # a lagged chain runs the emit kernel once per graph, the step kernel every step
+    dom = "step" if (lag or step_ms >= emit_ms) else "emit"
+    k = kern[dom]
+    other = kern["emit" if dom == "step" else "step"]
+    hbm_frac = k["gbs"] / HBM_PEAK_GBS
+    pkey = f"{'lag' if (lag and dom == 'step') else dom}:{cfg.scenario}:N{N}:B{B}"
+    pmc, note = pmc_entry(pkey)
+    valu = None
+    if pmc and pmc.get("valu_insts_per_launch"):
+        issue_us = pmc["valu_insts_per_launch"] * VALU_ISSUE_CYCLES / N_SIMDS / (CLOCK_GHZ * 1e3)
+        valu = dict(insts_per_launch=round(pmc["valu_insts_per_launch"]),
+                    insts_per_wave=round(pmc["valu_insts_per_launch"] / pmc["waves"], 1),
+                    issue_us=round(issue_us, 3), frac=round(issue_us / (k["ms"] * 1e3), 4),
+                    model=f"{VALU_ISSUE_CYCLES} cycles per wave64 VALU per SIMD x {N_SIMDS} SIMDs at "
+                          f"{CLOCK_GHZ} GHz (DESIGN.md §5)")
+    bound = "valu" if valu and valu["frac"] > hbm_frac else "hbm"
+    roofline = dict(kernel=k["kernel"], bound=bound, achieved=round(k["gbs"], 1), peak=HBM_PEAK_GBS,
+                    unit="GB/s", frac=round(hbm_frac, 4), hbm_frac=round(hbm_frac, 4),
+                    valu_frac=valu["frac"] if valu else None,
+                    traffic=round(pmc["hbm_bytes_per_launch"]) if pmc else None,
+                    pmc=dict(key=pkey, status=note, valu=valu,
+                             source=pmc.get("source") if pmc else None),
+                    algorithmic_bytes_per_launch=int(k["bytes"]), mean_launch_us=round(k["ms"] * 1e3, 3),
+                    timing=f"HIP events around {L} back-to-back graph launches of the kernel",
+                    other_kernel=dict(kernel=other["kernel"], achieved=round(other["gbs"], 1),
+                                      algorithmic_bytes_per_launch=int(other["bytes"]),
+                                      mean_launch_us=round(other["ms"] * 1e3, 3)))
+    log(f"kernels: {json.dumps(kern)}")
+    return roofline
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -27,6 +27,8 @@ struct gsm_handle {
     hipStream_t cap_stream = nullptr;
     int32_t *bsum_alt = nullptr;   // second half of the per-workgroup edge-sum double buffer (lagged emission)
     int32_t *block_order = nullptr;   // ragged mixed: workgroup -> env block, heaviest first
+    int32_t *order_host = nullptr;    // pinned staging of block_order's async upload
+    hipEvent_t order_copied = nullptr;   // recorded after the last upload (staging free again)
     struct Slot {
         hipGraph_t graph = nullptr;
         hipGraphExec_t exec = nullptr;
@@ -62,8 +64,11 @@ int align16(int x) { return (x + 15) & ~15; }
 // iterations), N_env for navigation; a block costs its heaviest env. The
 // order only schedules: every output is the same under any order (each
 // workgroup writes its own env block's slots). Recomputed when the seed that
-// draws the env shapes changes (a host-to-device copy then; never per step).
-int update_block_order(gsm_handle *h) {
+// draws the env shapes changes (never per step). The upload is stream-ordered
+// on the caller's stream `s` (from pinned staging), so kernels enqueued on it
+// before the reseed finish with the old order and every later one sees the new
+// order; the staging buffer is reused only after the previous upload read it.
+int update_block_order(gsm_handle *h, hipStream_t s) {
     const gsm::DevParams &p = h->dp;
     if (p.path != gsm::kPathRagged || p.scenario != gsm::kScnMixed) return GSM_OK;
     const int nb = h->sz.n_blocks, per = h->sz.envs_per_block;
@@ -82,14 +87,33 @@ int update_block_order(gsm_handle *h) {
     std::vector<int32_t> order(nb);
     for (int k = 0; k < nb; ++k) order[k] = k;
     std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key[a] > key[b]; });
+    const size_t bytes = (size_t)nb * sizeof(int32_t);
     hipError_t e = hipSuccess;
-    if (!h->block_order) e = hipMalloc(&h->block_order, (size_t)nb * sizeof(int32_t));
-    if (e != hipSuccess) {
-        h->block_order = nullptr;
-        return hip_fail(h, e, "hipMalloc (block order)");
+    if (!h->block_order) {
+        e = hipMalloc(&h->block_order, bytes);
+        if (e != hipSuccess) {
+            h->block_order = nullptr;
+            return hip_fail(h, e, "hipMalloc (block order)");
+        }
+        e = hipHostMalloc((void **)&h->order_host, bytes, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            h->order_host = nullptr;
+            return hip_fail(h, e, "hipHostMalloc (block order staging)");
+        }
+        e = hipEventCreateWithFlags(&h->order_copied, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            h->order_copied = nullptr;
+            return hip_fail(h, e, "hipEventCreate (block order)");
+        }
+    } else {
+        e = hipEventSynchronize(h->order_copied);   // the previous upload has read the staging
+        if (e != hipSuccess) return hip_fail(h, e, "hipEventSynchronize (block order)");
     }
-    e = hipMemcpy(h->block_order, order.data(), (size_t)nb * sizeof(int32_t), hipMemcpyHostToDevice);
-    if (e != hipSuccess) return hip_fail(h, e, "hipMemcpy (block order)");
+    memcpy(h->order_host, order.data(), bytes);
+    e = hipMemcpyAsync(h->block_order, h->order_host, bytes, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return hip_fail(h, e, "hipMemcpyAsync (block order)");
+    e = hipEventRecord(h->order_copied, s);
+    if (e != hipSuccess) return hip_fail(h, e, "hipEventRecord (block order)");
     h->dp.block_order = h->block_order;
     return GSM_OK;
 }
@@ -380,8 +404,10 @@ int gsm_bind(gsm_handle *h, const gsm_buffers *b) {
     if (ragged) {
         const hipError_t e = gsm::upload_ragged_tables();
         if (e != hipSuccess) return hip_fail(h, e, "ragged constant tables");
-        const int rc = update_block_order(h);
+        const int rc = update_block_order(h, nullptr);
         if (rc) return rc;
+        const hipError_t es = hipStreamSynchronize(nullptr);   // bind is not stream-ordered
+        if (es != hipSuccess) return hip_fail(h, es, "hipStreamSynchronize (block order)");
     }
     if (((uintptr_t)b->pos | (uintptr_t)b->vel | (uintptr_t)b->ep_acc | (uintptr_t)b->ep_last) & 7)
         return fail(h, GSM_EINVAL, "pos/vel/ep_acc/ep_last must be 8-byte aligned");
@@ -418,7 +444,7 @@ int gsm_reset(gsm_handle *h, uint64_t seed, int reseed, const uint8_t *env_mask,
         h->dp.seed_hi = (uint32_t)(seed >> 32);
         drop_graph(h);   // captured auto-resets would use the old key
         if (h->bound) {
-            const int rc = update_block_order(h);   // mixed: the env shapes follow the seed
+            const int rc = update_block_order(h, as_stream(stream));   // mixed: the env shapes follow the seed
             if (rc) return rc;
         }
     }
@@ -681,7 +707,10 @@ int gsm_destroy(gsm_handle *h) {
     drop_graph(h);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->bsum_alt) (void)hipFree(h->bsum_alt);
+    if (h->order_copied) (void)hipEventSynchronize(h->order_copied);
     if (h->block_order) (void)hipFree(h->block_order);
+    if (h->order_host) (void)hipHostFree(h->order_host);
+    if (h->order_copied) (void)hipEventDestroy(h->order_copied);
     delete h;
     return GSM_OK;
 }

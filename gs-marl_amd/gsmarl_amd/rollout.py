@@ -143,13 +143,20 @@ class GraphRolloutBuffer:
     def graph_batch(self, t_idx: torch.Tensor, b_idx: torch.Tensor) -> dict:
         """PyG-style batch of K samples (slot t_idx[k], env b_idx[k]): node_feat
         [K*E, 7], edge_index [2, sum] int64 with local ids k*E + e, edge_attr,
-        batch [K*E] (sample of each node), ptr [K+1] (edge offsets)."""
+        batch [K*E] (sample of each node), ptr [K+1] (edge offsets).
+        Raises ValueError if a requested sample's edges were truncated because
+        its slot overflowed the per-slot edge capacity (``overflowed()``)."""
         E = self.E
         t = t_idx.to(self.edge_ptr.device, torch.int64)
         b = b_idx.to(self.edge_ptr.device, torch.int64)
         K = t.numel()
         start = self.edge_ptr[t, b]
-        cnt = self.edge_ptr[t, b + 1] - start
+        end = self.edge_ptr[t, b + 1]
+        if bool((end > self.cap).any()):
+            raise ValueError(f"graph_batch: a requested sample's edges run past the slot capacity {self.cap} "
+                             "(the slot overflowed and was truncated); size the buffer with a larger edge "
+                             "capacity")
+        cnt = end - start
         ptr = torch.zeros(K + 1, dtype=torch.int64, device=t.device)
         torch.cumsum(cnt, 0, out=ptr[1:])
         total = int(ptr[-1].item())

@@ -91,6 +91,13 @@ def test_edge_overflow_is_truncated():
     assert torch.equal(buf.edge_ptr[0], out["edge_ptr"])                 # true offsets kept
     cap = buf.cap
     assert torch.equal(buf.edge_index[0], out["edge_index"][:, :cap])    # the prefix that fits
+    # sampling a truncated env is a clear error, not a device-side index assert
+    last = torch.tensor([31])
+    with pytest.raises(ValueError, match="capacity"):
+        buf.graph_batch(torch.tensor([0]), last)
+    fits = int((buf.edge_ptr[0, 1:] <= cap).nonzero()[0].item()) if bool((buf.edge_ptr[0, 1:] <= cap).any()) else None
+    if fits is not None:
+        buf.graph_batch(torch.tensor([0]), torch.tensor([fits]))
     env.close()
     ref.close()
 

@@ -1,7 +1,12 @@
-"""Merge tools/pmc.sh summaries into profiles/pmc_traffic.json, the file
-bench.py reads for roofline.traffic: HBM bytes per launch of each kernel =
-2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes; the x2 is the gfx950 FETCH_SIZE
-correction of MI355X_MICROARCH.md section HBM/rocprofv3).
+"""Merge tools/pmc.sh summaries into profiles/pmc_kernels.json, the file
+bench.py reads for roofline.traffic and roofline.valu_frac.
+
+Per kernel: HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes;
+the x2 is the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md section
+HBM/rocprofv3), VALU / SALU / LDS instructions per launch and waves. The file
+records the hash of the kernel sources it was collected on (bench.kernel_src_hash);
+bench.py ignores it once the sources change, so stale counters never reach a
+bench line.
 
 Usage: python tools/pmc_traffic.py OUT_JSON [KINDS@]KEY_PREFIX=SUMMARY_DIR ...
   e.g. h:navigation:N24:B8192=gpurun_out/pmc_h  (keys: step:navigation:N24:B8192, emit:...)
@@ -10,9 +15,19 @@ Usage: python tools/pmc_traffic.py OUT_JSON [KINDS@]KEY_PREFIX=SUMMARY_DIR ...
 import json
 import os
 import sys
+import time
+from pathlib import Path
+
+sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
+from bench import kernel_src_hash  # noqa: E402
 
 out_path = sys.argv[1]
+h = kernel_src_hash()
 res = json.load(open(out_path)) if os.path.exists(out_path) else {}
+if res.get("src_hash") != h:   # entries from other sources are dropped, not mixed
+    res = {}
+res.update(src_hash=h, collected=time.strftime("%Y-%m-%d %H:%M:%S"))
+ent = res.setdefault("entries", {})
 for spec in sys.argv[2:]:
     key, d = spec.split("=", 1)
     kinds = None
@@ -29,9 +44,14 @@ for spec in sys.argv[2:]:
             continue
         rd = 2 * c["FETCH_SIZE"] * 1024
         wr = c["WRITE_SIZE"] * 1024
-        res[f"{kern}:{key.split(':', 1)[1]}"] = dict(
-            hbm_bytes_per_launch=round(rd + wr), read_bytes_corrected=round(rd), write_bytes=round(wr),
-            fetch_size_kib=c["FETCH_SIZE"], write_size_kib=c["WRITE_SIZE"], dispatches=v["dispatches"],
-            source=d)
+        e = dict(hbm_bytes_per_launch=round(rd + wr), read_bytes_corrected=round(rd), write_bytes=round(wr),
+                 fetch_size_kib=c["FETCH_SIZE"], write_size_kib=c["WRITE_SIZE"], dispatches=v["dispatches"],
+                 source=d)
+        for cn, k in (("SQ_INSTS_VALU", "valu_insts_per_launch"), ("SQ_INSTS_SALU", "salu_insts_per_launch"),
+                      ("SQ_INSTS_LDS", "lds_insts_per_launch"), ("SQ_WAVES", "waves"),
+                      ("SQ_WAVE_CYCLES", "wave_quad_cycles_per_launch")):
+            if cn in c:
+                e[k] = c[cn]
+        ent[f"{kern}:{key.split(':', 1)[1]}"] = e
 json.dump(res, open(out_path, "w"), indent=1, sort_keys=True)
 print(json.dumps(res, indent=1))
