@@ -241,6 +241,7 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
     p->seed_lo = (uint32_t)(c->seed & 0xFFFFFFFFull);
     p->seed_hi = (uint32_t)(c->seed >> 32);
     p->env_base = c->env_base;
+    p->strict = c->strict_degenerate != 0;
     if (p->path == gsm::kPathRagged) {
         // assignment cost matrix [N][N] fp32 + staged entity positions [E]
         p->wave_lds_step = align16(4 * N * N + 8 * p->E);
@@ -251,10 +252,11 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
         // one env per wave: + the staged edge list (emit_rows_staged)
         p->wave_lds_emit = align16(p->G == 1 ? 36 * p->E : 8 * p->G * p->E);
     } else {
-        // tile: whole-workgroup LDS: positions, velocities, new positions, costs, reductions;
+        // tile: whole-workgroup LDS: positions, velocities, new positions, costs, reductions,
+        // the two degenerate-state flags;
         // + the symmetric sweep's column pairs, agent-row words and obstacle-row
         // agent bits when they fit in 32 KB (gsm_tile_kernels.hip: obs_sweep_sym)
-        p->wave_lds_step = align16(8 * p->E + 8 * N + 8 * N + 4 * N + 8 * (gsm::kTileBlock / gsm::kWave));
+        p->wave_lds_step = align16(8 * p->E + 8 * N + 8 * N + 4 * N + 8 * (gsm::kTileBlock / gsm::kWave) + 8);
         const int sym = 16 * ((N + 1) / 2) + 16 * N * p->W + 8 * No * p->W + 16;
         p->tile_sym = sym <= 32768;
         if (p->tile_sym) p->wave_lds_step += sym;
@@ -431,6 +433,7 @@ int gsm_bind(gsm_handle *h, const gsm_buffers *b) {
     p.contact_mask = b->contact_mask;
     p.env_shape = b->env_shape;
     p.assign = b->assign;
+    p.degenerate = b->degenerate;
     h->bound = true;
     drop_graph(h);   // a captured graph holds the old pointers
     return GSM_OK;

@@ -138,6 +138,28 @@ __device__ __forceinline__ float2 action_force(const DevParams &p, int64_t a) {
     return make_float2(ux * p.sens, uy * p.sens);
 }
 
+// App. A S16 (degenerate states). nonfinite2: a position with a NaN/inf
+// coordinate. strict_bad: in strict mode, whether agent `a`'s contact force is
+// NaN as in MPE — a collider c != self at d2 = 0 (MPE: delta / dist = 0 / 0)
+// or any agent of the env at a non-finite position (MPE evaluates every pair,
+// so one NaN agent reaches every agent's force). `pos_of(c)` gives collider
+// c's position (agents first); O(M) per agent — strict mode is a checking
+// mode, the default path never runs it.
+constexpr uint8_t kDegCoincident = 1, kDegNonfinite = 2;   // gsm.h GSM_DEGENERATE_*
+__device__ __forceinline__ bool nonfinite2(float2 a) {
+    return !(__builtin_isfinite(a.x) && __builtin_isfinite(a.y));
+}
+template <typename PosOf>
+__device__ __forceinline__ bool strict_bad(int self, float2 a, int N, int M, PosOf pos_of) {
+    bool bad = nonfinite2(a);
+    for (int c = 0; c < M; ++c) {
+        const float2 q = pos_of(c);
+        const float dx = a.x - q.x, dy = a.y - q.y;
+        bad |= (c != self && dx * dx + dy * dy == 0.0f) || (c < N && nonfinite2(q));
+    }
+    return bad;
+}
+
 // MPE get_collision_force magnitude / d for one pair inside the cutoff:
 //   F/d = c * k * softplus(-(d - dmin)/k) / d.
 // Written as pen = max(D, 0) + k*log1p(exp(-|D|/k)), D = dmin - d: the

@@ -35,6 +35,7 @@ struct DevParams {
     int32_t nf_full;       // write every node-feature row (redirected outputs)
     int32_t G;             // envs per wave (segmented path), 1 otherwise
     int32_t tile_sym;      // tile path: symmetric sweep (its LDS fits), gsm_tile_kernels.hip
+    int32_t strict;        // App. A S16 strict mode: coincident-pair / NaN forces as in MPE
     uint32_t seed_lo, seed_hi;
     int64_t env_base;
     int32_t wave_lds_step, wave_lds_emit;      // bytes of LDS per wave
@@ -56,6 +57,7 @@ struct DevParams {
     uint64_t *contact_mask;   // [B][N] contact candidates (segmented path)
     int32_t *env_shape;       // [B] ragged: N_env | scenario << 8
     int32_t *assign;          // [B][N] ragged: LSA slot per agent
+    uint8_t *degenerate;      // [B] optional: GSM_DEGENERATE_* bits of the launch's final state
     const int32_t *block_order;   // ragged mixed: workgroup -> env block, heaviest first (nullptr: identity)
     int64_t edge_capacity;
     const void *actions;

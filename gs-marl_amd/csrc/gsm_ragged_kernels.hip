@@ -163,6 +163,13 @@ __device__ __forceinline__ float2 slot_of(const DevParams &p, const RShape &s, i
 // lane's column (row `lane`), and its cost in *own.
 __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, float *own, int *iters = nullptr) {
     const bool col = lane < N;
+    // a non-finite agent position (strict mode, App. A S16; or a caller-written
+    // state) has no assignment (scipy raises on such a cost matrix): slot -1,
+    // cost NaN
+    if (__any(col && nonfinite2(pa))) {
+        *own = __builtin_nanf("");
+        return -1;
+    }
 #ifdef GSM_ABL_NO_LSA   // timing-only ablation: identity assignment
     *own = 0.0f;
     return col ? lane : -1;
@@ -339,6 +346,13 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
                 Fy += f * dy;
             }
         }
+        if (p.strict) {   // App. A S16 strict: MPE's 0/0 force (every lane runs the readlanes)
+            const bool bad = strict_bad(lane, cp, s.N, s.M, [&](int c) { return rl_f2(cp, c); });
+            if (lane < s.N && bad) {
+                Fx = __builtin_nanf("");
+                Fy = __builtin_nanf("");
+            }
+        }
         if (lane < s.N) {
             v.x = v.x * p.omd;
             v.y = v.y * p.omd;
@@ -359,9 +373,13 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
     }
 
     // collision cost (agent lanes) and radius row masks (collider lanes)
+    // (+ coinc: a collider other than the lane's own at d2 = 0 with an agent
+    // on either side, App. A S16)
+    bool coinc = false;
     auto pair_sweep = [&](int *cnt) {
         uint64_t rm = 0;
         int n = 0;
+        bool z = false;
         for (int c = 0; c < s.M; ++c) {
             const float2 q = rl_f2(cp, c);
             const float dx = cp.x - q.x, dy = cp.y - q.y;
@@ -369,8 +387,10 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
             const bool other = c != lane;
             n += (other && d2 < (c < s.N ? p.dmin2_aa : p.dmin2_ao)) ? 1 : 0;
             rm |= (other && d2 > 0.0f && d2 <= p.R2) ? (1ull << c) : 0ull;
+            z |= other && d2 == 0.0f && c < s.N;
         }
         *cnt = n;
+        coinc = __any(lane < s.M && z);
         return lane < s.M ? rm : 0ull;
     };
     int cnt = 0;
@@ -479,7 +499,10 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
 
     if (lane < s.M) p.row_mask[eb * Mmax + lane] = rmask;
     const int edges = wave_sum((int)__popcll(rmask)) + 2 * s.N * s.Tper;
+    const bool nonfin = __any(lane < s.N && nonfinite2(cp));
     if (lane == 0) {
+        if (p.degenerate)
+            p.degenerate[b] = (uint8_t)((coinc ? kDegCoincident : 0) | (nonfin ? kDegNonfinite : 0));
         p.step_count[b] = t;
         p.episode[b] = ep;
         p.ep_acc[b] = acc;

@@ -171,7 +171,7 @@ __device__ __forceinline__ uint32_t pack_lo16(uint64_t a, uint64_t b) {
 template <int kN, int kNo>
 __device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, const float2 *sp, float *s_xy,
                                              float2 pm, bool full, uint64_t oo, uint64_t &row, uint64_t &cand,
-                                             int &ccnt) {
+                                             int &ccnt, bool &coinc) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     constexpr int N = kN, M = kN + kNo;
     static_assert(M > 32 && M <= 64 && N <= 32 && N % 2 == 0, "one env per wave, agent bits in the low word");
@@ -269,7 +269,8 @@ __device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, 
             }
         }
     }
-    if (__builtin_expect(__any(coincident), 0)) {
+    coinc = __any(coincident);   // the env (= the wave) holds a coincident pair (App. A S16)
+    if (__builtin_expect(coinc, 0)) {
         // exact agent-column bits of every row (and obstacle columns of agent
         // rows): rad' also holds coincident pairs
         uint64_t ex = 0;
@@ -289,14 +290,15 @@ __device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, 
 
 // Observation sweep (file header). row/cand/ccnt are per lane: row = radius
 // row mask (compact bits), cand = contact candidates (agent lanes),
-// ccnt = collisions of agent lanes (self excluded). With full = false the
-// obstacle-obstacle bits are taken from `oo` (the cached masks).
+// ccnt = collisions of agent lanes (self excluded), coinc = the lane's env
+// holds a coincident pair with an agent (d2 = 0, App. A S16). With full =
+// false the obstacle-obstacle bits are taken from `oo` (the cached masks).
 template <int kN, int kNo, int kG>
 __device__ __forceinline__ void obs_sweep(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L,
                                           const float2 *sp, float *s_xy, float2 pm, bool full, uint64_t oo,
-                                          uint64_t &row, uint64_t &cand, int &ccnt) {
+                                          uint64_t &row, uint64_t &cand, int &ccnt, bool &coinc) {
     if constexpr (kG == 1 && kN > 0 && kN <= 32 && kN % 2 == 0 && kN + kNo > 32) {
-        obs_sweep_g1<kN, kNo>(p, L, sp, s_xy, pm, full, oo, row, cand, ccnt);
+        obs_sweep_g1<kN, kNo>(p, L, sp, s_xy, pm, full, oo, row, cand, ccnt, coinc);
         return;
     }
     const int N = s.N, M = s.M;
@@ -315,6 +317,13 @@ __device__ __forceinline__ void obs_sweep(const DevParams &p, const Shape<kN, kN
     uint64_t c = 0;
     OwnBits<kN> own = 0;                                    // per-lane agent bits (obstacle rows)
     int cc = 0;
+    // lanes at d2 = 0 from an agent column other than their own row (wave-
+    // uniform, scalar ops only): b_col holds d2 < dmin2 (self and coincident
+    // pairs included), b_cand 0 < d2 < cut2 with cut2 > dmin2, so
+    // b_col & ~b_cand is exactly d2 = 0; the self lanes of column j are the
+    // segments' lanes j
+    uint64_t zero = 0, selves = 0;
+    for (int g = 0; g < (kG == 1 ? 1 : s.G); ++g) selves |= 1ull << (g * M);
 #pragma unroll 4
     for (int j = 0; j < N; ++j) {
         const float2 q = sp[j];
@@ -326,6 +335,7 @@ __device__ __forceinline__ void obs_sweep(const DevParams &p, const Shape<kN, kN
         const uint64_t b_cand = __ballot(t < cutb);
         const uint64_t b_col = __ballot(d2 < dmin2);
         own |= (OwnBits<kN>)rad << j;
+        zero |= b_col & ~b_cand & ~(selves << j);
         r = capture<kG>(b_rad, j, L, segmask, r);
         c = capture<kG>(b_cand, j, L, segmask, c);
         cc = capture_count<kG>(b_col, j, L, segmask, cc);
@@ -343,7 +353,8 @@ __device__ __forceinline__ void obs_sweep(const DevParams &p, const Shape<kN, kN
     }
     row = r;
     cand = c;
-    ccnt = cc - 1;                                          // the self pair (d2 = 0 < dmin2)
+    ccnt = cc - (nonfinite2(pm) ? 0 : 1);                   // the self pair (d2 = 0 < dmin2; NaN if pm is not finite)
+    coinc = ((zero >> L.base) & segmask) != 0;
 }
 
 // Environment._set_action for a compile-time action format (kFmt < 0: runtime)
@@ -807,6 +818,10 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
                 Fx += f * dx;
                 Fy += f * dy;
             }
+            if (p.strict && strict_bad(m, pi, N, M, [&](int c) { return s_pos[row_entity(c, N)]; })) {
+                Fx = __builtin_nanf("");   // App. A S16 strict: MPE's 0/0 force
+                Fy = __builtin_nanf("");
+            }
             v.x = v.x * p.omd;
             v.y = v.y * p.omd;
             v.x = v.x + (Fx * p.inv_mass) * p.dt;
@@ -834,11 +849,12 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     float2 pm = s_pos[row_entity(m, N)];
     uint64_t row, cand;
     int ccnt;
+    bool coinc;
 #ifdef GSM_ABL_NO_SWEEP   // timing-only
-    row = oo; cand = 0; ccnt = 0;
+    row = oo; cand = 0; ccnt = 0; coinc = false;
     asm volatile("" :: "v"(pm.x), "v"(pm.y));
 #else
-    obs_sweep<kN, kNo, kG>(p, s, L, s_pos, s_nf, pm, full, oo, row, cand, ccnt);
+    obs_sweep<kN, kNo, kG>(p, s, L, s_pos, s_nf, pm, full, oo, row, cand, ccnt, coinc);
 #endif
     GSM_STAMP(p, wid, 4);
 
@@ -873,11 +889,13 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
             const float2 pm2 = s_pos[row_entity(m, N)];
             uint64_t row2, cand2;
             int cc2;
-            obs_sweep<kN, kNo, kG>(p, s, L, s_pos, s_nf, pm2, true, 0ull, row2, cand2, cc2);
+            bool coinc2;
+            obs_sweep<kN, kNo, kG>(p, s, L, s_pos, s_nf, pm2, true, 0ull, row2, cand2, cc2, coinc2);
             if (reset) {
                 pm = pm2;
                 row = row2;
                 cand = cand2;
+                coinc = coinc2;
             }
             relaid = reset;
         }
@@ -933,6 +951,14 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     emit_rows<kN, kNo, kG>(s, L, s_pos, row, (int64_t)(L.live ? L.b : 0) * (p.edge_capacity / p.B),
                            EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity});
 #endif
+    // App. A S16 flags of the final state: a coincident pair (from the sweep),
+    // an agent at a non-finite position
+    uint8_t deg = 0;
+    if (p.degenerate) {
+        const uint64_t nb = __ballot(L.agent && nonfinite2(pm));
+        const uint64_t segm = M >= 64 ? ~0ull : ((1ull << M) - 1);
+        deg = (uint8_t)((coinc ? kDegCoincident : 0) | (((nb >> L.base) & segm) ? kDegNonfinite : 0));
+    }
     // edge count (radius rows + goal edges both ways)
     const int edges = __popcll(row) + ((L.live && m == 0) ? 2 * N : 0);
     int wave_edges;
@@ -944,6 +970,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
             p.ep_acc[L.b] = acc;
             p.done[L.b] = done ? 1 : 0;
             p.edge_count[L.b] = wave_edges;
+            if (p.degenerate) p.degenerate[L.b] = deg;
         }
     } else {
         wave_edges = wave_sum(edges);
@@ -954,6 +981,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
             p.ep_acc[L.b] = acc;
             p.done[L.b] = done ? 1 : 0;
             p.edge_count[L.b] = env_edges;
+            if (p.degenerate) p.degenerate[L.b] = deg;
         }
     }
     GSM_STAMP(p, wid, 7);

@@ -68,7 +68,7 @@ __device__ __forceinline__ float tile_sum(float v, float *s_red) {
 // agent collision counts in s_cost.
 template <int kW>   // mask words per row; 0 = runtime p.W
 __device__ __forceinline__ int obs_sweep(const DevParams &p, const float2 *s_pos, int *s_cost, int64_t eb,
-                                         bool keep_oo) {
+                                         bool keep_oo, int *s_coinc) {
     const int N = p.N, M = p.M, W = kW > 0 ? kW : p.W;
     constexpr int kR = kW > 0 ? kW : 1;     // words held in registers per pass
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -84,6 +84,7 @@ __device__ __forceinline__ int obs_sweep(const DevParams &p, const float2 *s_pos
     // column (d2 = 0) by themselves; lanes past M hold an infinite position.
     const uint32_t R2b = (uint32_t)__float_as_int(p.R2);
     int pairs = 0;   // per lane: set bits of the words it stores / keeps
+    bool zc = false;   // an agent row with a collider other than itself at d2 = 0 (App. A S16)
     for (int g0 = 0; g0 < rows_w; g0 += kWave) {
         const int ng = min(kWave, rows_w - g0);
         const int ja = min(ng, max(0, arows_w - g0));   // rows [0, ja) of the group are agent rows
@@ -121,6 +122,9 @@ __device__ __forceinline__ int obs_sweep(const DevParams &p, const float2 *s_pos
                     const uint64_t rad = __builtin_amdgcn_ballot_w64(tb < R2b);
                     const uint64_t con = __builtin_amdgcn_ballot_w64(tb < cutb[u]);
                     ncol += (uint32_t)__popcll(__builtin_amdgcn_ballot_w64(d2 < dmin2[u]));
+                    const int rj = wave + kTileWaves * (g0 + j), cb = 64 * (k0 + u);
+                    const uint64_t self = (rj >= cb && rj < cb + 64) ? 1ull << (rj - cb) : 0ull;
+                    zc |= (__builtin_amdgcn_ballot_w64(d2 == 0.0f) & ~self) != 0;
                     rad_lo[u] = writelane_u32((uint32_t)rad, (uint32_t)j, rad_lo[u]);
                     rad_hi[u] = writelane_u32((uint32_t)(rad >> 32), (uint32_t)j, rad_hi[u]);
                     con_lo[u] = writelane_u32((uint32_t)con, (uint32_t)j, con_lo[u]);
@@ -155,8 +159,9 @@ __device__ __forceinline__ int obs_sweep(const DevParams &p, const float2 *s_pos
                 }
             }
         }
-        if (lane < ja) s_cost[rl] = (int)cnt - 1;   // minus the row's own column
+        if (lane < ja) s_cost[rl] = (int)cnt - (nonfinite2(rowp) ? 0 : 1);   // minus the row's own column (NaN row: d2 NaN)
     }
+    if (zc) *s_coinc = 1;
     return pairs;
 }
 
@@ -324,12 +329,12 @@ __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s
 }
 
 __device__ __forceinline__ int obs_sweep_any(const DevParams &p, const float2 *s_pos, int *s_cost, int64_t eb,
-                                             bool keep_oo) {
+                                             bool keep_oo, int *s_coinc) {
     switch (p.W) {
-        case 2: return obs_sweep<2>(p, s_pos, s_cost, eb, keep_oo);
-        case 3: return obs_sweep<3>(p, s_pos, s_cost, eb, keep_oo);
-        case 4: return obs_sweep<4>(p, s_pos, s_cost, eb, keep_oo);
-        default: return obs_sweep<0>(p, s_pos, s_cost, eb, keep_oo);
+        case 2: return obs_sweep<2>(p, s_pos, s_cost, eb, keep_oo, s_coinc);
+        case 3: return obs_sweep<3>(p, s_pos, s_cost, eb, keep_oo, s_coinc);
+        case 4: return obs_sweep<4>(p, s_pos, s_cost, eb, keep_oo, s_coinc);
+        default: return obs_sweep<0>(p, s_pos, s_cost, eb, keep_oo, s_coinc);
     }
 }
 
@@ -429,10 +434,11 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
     int *s_cost = (int *)(s_np + N);          // [N]
     int *s_ired = s_cost + N;                 // [kTileWaves]
     float *s_fred = (float *)(s_ired + kTileWaves);
+    int *s_deg = (int *)(s_fred + kTileWaves);   // [2] coincident pair (unsymmetric sweep), non-finite agent
     // symmetric sweep scratch (p.tile_sym), 16-byte aligned after the above
     TileSymLds sym;
     {
-        unsigned char *q = smem + ((8 * E + 8 * N + 8 * N + 4 * N + 8 * kTileWaves + 15) & ~15);
+        unsigned char *q = smem + ((8 * E + 8 * N + 8 * N + 4 * N + 8 * kTileWaves + 8 + 15) & ~15);
         sym.xy = (float *)q;
         q += 16 * ((N + 1) / 2);
         sym.arow = (uint64_t *)q;
@@ -464,6 +470,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
     float2 acc = p.ep_acc[b];
     const bool do_reset = p.mode == kModeReset && (p.env_mask == nullptr || p.env_mask[b] != 0);
     bool relaid = false;
+    if (tid == 0) s_deg[0] = s_deg[1] = 0;
     __syncthreads();
 
     auto relayout = [&]() {   // scenario.reset_world with the Philox layout
@@ -472,6 +479,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
         acc = make_float2(0.0f, 0.0f);
         const uint32_t gid = (uint32_t)(p.env_base + b);
         __syncthreads();
+        if (tid == 0) s_deg[0] = 0;   // the flags describe the new layout
         for (int e = tid; e < E; e += kTileBlock) s_pos[e] = layout_pos(p, gid, (uint32_t)ep, (uint32_t)e);
         for (int i = tid; i < N; i += kTileBlock) s_vel[i] = make_float2(0.0f, 0.0f);
         relaid = true;
@@ -506,7 +514,11 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
             for (int k = 0; k < kPre; ++k)
                 if (k < W) visit(k, pre ? cw[k] : cm[(int64_t)i * W + k]);
             for (int k = kPre; k < W; ++k) visit(k, cm[(int64_t)i * W + k]);
-            const float Fx = u.x + fx, Fy = u.y + fy;
+            float Fx = u.x + fx, Fy = u.y + fy;
+            if (p.strict && strict_bad(i, pi, N, p.M, [&](int c) { return s_pos[collider_entity(c, N)]; })) {
+                Fx = __builtin_nanf("");   // App. A S16 strict: MPE's 0/0 force
+                Fy = __builtin_nanf("");
+            }
             float2 v = s_vel[i];
             v.x = v.x * p.omd;
             v.y = v.y * p.omd;
@@ -532,7 +544,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
     // observation sweep of the post-step state: masks, collision counts, pairs
 #ifndef GSM_ABL_NO_SWEEP
     int pairs = p.tile_sym ? obs_sweep_sym(p, s_pos, sym, s_cost, eb, p.mode == kModeStep && !relaid)
-                           : obs_sweep_any(p, s_pos, s_cost, eb, p.mode == kModeStep && !relaid);
+                           : obs_sweep_any(p, s_pos, s_cost, eb, p.mode == kModeStep && !relaid, s_deg);
 #else
     int pairs = 0;
     for (int i = tid; i < N; i += kTileBlock) s_cost[i] = 0;
@@ -564,10 +576,13 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
             if (tid == 0) p.ep_last[b] = acc;
             relayout();
             pairs = p.tile_sym ? obs_sweep_sym(p, s_pos, sym, s_cost, eb, false)
-                               : obs_sweep_any(p, s_pos, s_cost, eb, false);
+                               : obs_sweep_any(p, s_pos, s_cost, eb, false, s_deg);
         }
     }
-    pairs = tile_sum(pairs, s_ired);
+    if (p.degenerate)
+        for (int i = tid; i < N; i += kTileBlock)
+            if (nonfinite2(s_pos[i])) s_deg[1] = 1;
+    pairs = tile_sum(pairs, s_ired);   // (its barriers also publish s_deg)
 
     // node features [E][7] = [vx vy px py gx-px gy-py type]: agent rows every
     // step (one thread per row), goal/obstacle rows only on layout change
@@ -617,6 +632,10 @@ skip_nf:
         p.done[b] = done ? 1 : 0;
         p.edge_count[b] = edges;
         p.block_edge_sum[b] = edges;
+        if (p.degenerate) {
+            const int co = p.tile_sym ? *sym.flag : s_deg[0];
+            p.degenerate[b] = (uint8_t)((co ? kDegCoincident : 0) | (s_deg[1] ? kDegNonfinite : 0));
+        }
     }
 }
 

@@ -11,7 +11,8 @@ import os
 from pathlib import Path
 
 LIB_PATH = Path(os.environ.get("GSM_LIB_PATH") or Path(__file__).resolve().parent / "lib" / "libgsm.so")
-ABI_VERSION = 4
+ABI_VERSION = 5
+DEGENERATE_COINCIDENT, DEGENERATE_NONFINITE = 1, 2
 
 GSM_OK, GSM_EINVAL, GSM_EHIP, GSM_ESTATE = 0, -1, -2, -3
 GRAPH_SLOTS = 4
@@ -33,6 +34,7 @@ class GsmConfig(C.Structure):
         ("agent_size", C.c_float), ("goal_size", C.c_float), ("obstacle_size", C.c_float),
         ("sense_radius", C.c_float), ("contact_cutoff", C.c_float),
         ("n_agents_min", C.c_int32), ("formation_radius", C.c_float),
+        ("strict_degenerate", C.c_int32),
     ]
 
 
@@ -47,7 +49,7 @@ class GsmSizes(C.Structure):
 
 BUFFER_FIELDS = ["pos", "vel", "step_count", "episode", "ep_acc", "ep_last", "node_feat",
                  "reward", "cost", "done", "edge_count", "block_edge_sum", "edge_ptr",
-                 "edge_index", "edge_attr", "row_mask", "contact_mask", "env_shape", "assign"]
+                 "edge_index", "edge_attr", "row_mask", "contact_mask", "env_shape", "assign", "degenerate"]
 
 
 class GsmBuffers(C.Structure):
@@ -141,6 +143,7 @@ def make_config(cfg) -> GsmConfig:
               "sense_radius", "contact_cutoff", "formation_radius"):
         setattr(c, f, float(getattr(cfg, f)))
     c.n_agents_min = int(cfg.n_agents_min)
+    c.strict_degenerate = int(bool(getattr(cfg, "strict_degenerate", False)))
     return c
 
 

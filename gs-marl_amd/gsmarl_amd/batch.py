@@ -10,6 +10,7 @@ stream provider only); every compute call goes through the C ABI. Layout
     node_feat  [B, E, 7] f32   vx vy px py gx-px gy-py type
     obs        [B, N, 6]       = node_feat[:, :N, :6]  (a view: MPE obs order)
     reward     [B, N] f32, cost [B, N] f32 (exact counts), done [B] u8
+    degenerate [B] u8      App. A S16 flags: 1 coincident collider pair, 2 non-finite agent
     edge_ptr   [B+1] i64; edge_index [2, cap] i32 (global node ids b*E+e),
     edge_attr  [cap] f32 (distance); valid prefix = edge_ptr[B]
 """
@@ -73,6 +74,8 @@ class GpuBatchEnv:
             # ragged batches: N_env | scenario << 8, and the LSA slot of each agent
             env_shape=torch.zeros(B, dtype=i32, device=dev),
             assign=torch.full((B, N), -1, dtype=i32, device=dev),
+            # App. A S16 flags per env (GSM_DEGENERATE_*: 1 coincident pair, 2 non-finite agent)
+            degenerate=torch.zeros(B, dtype=torch.uint8, device=dev),
         )
         bufs = _lib.GsmBuffers(**{k: self.t[k].data_ptr() for k in _lib.BUFFER_FIELDS})
         _lib.check(self.lib, self.lib.gsm_bind(self._h, C.byref(bufs)), self._h, "gsm_bind")
@@ -102,7 +105,7 @@ class GpuBatchEnv:
         t = self.t
         out = dict(obs=t["node_feat"][:, : self.N, :6], node_feat=t["node_feat"],
                    agent_id=self.agent_id, reward=t["reward"], cost=t["cost"], done=t["done"],
-                   edge_ptr=t["edge_ptr"])
+                   edge_ptr=t["edge_ptr"], degenerate=t["degenerate"])
         if self.cfg.ragged:
             out["assign"] = t["assign"]
             out["n_agents_env"] = t["env_shape"] & 0xFF

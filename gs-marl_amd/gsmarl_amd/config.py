@@ -38,6 +38,7 @@ class EnvConfig:
     contact_cutoff: float = 40.0           # in contact margins
     n_agents_min: int = 3                  # mixed: N_env drawn from [n_agents_min, n_agents]
     formation_radius: float = 0.5          # polygon N-gon radius (readme.md:89)
+    strict_degenerate: bool = False        # App. A S16: MPE's NaN for d = 0 pairs instead of the guard
 
     def __post_init__(self):
         if self.scenario not in SCENARIOS:

@@ -109,17 +109,26 @@ class MultiAgentEnv:
         return np.repeat(d[:, None], self.n, axis=1)
 
     def _info(self, out, cost=None):
+        """Per-agent info dicts: the cost (Constrain variants) and, when the
+        env is in a degenerate state (App. A S16: coincident colliders, or a
+        non-finite agent under strict_degenerate), ``degenerate`` = its flags."""
+        deg = out["degenerate"].cpu().numpy()
         if self.num_envs == 1:
             infos = [{} for _ in range(self.n_active)]
             if cost is not None:
                 for i, c in enumerate(cost):
                     infos[i]["cost"] = c
+            if deg[0]:
+                for info in infos:
+                    info["degenerate"] = int(deg[0])
             return infos
         infos = [[{} for _ in range(self.n)] for _ in range(self.num_envs)]
-        if cost is not None:
-            for b in range(self.num_envs):
-                for i in range(self.n):
+        for b in range(self.num_envs):
+            for i in range(self.n):
+                if cost is not None:
                     infos[b][i]["cost"] = float(cost[b, i, 0])
+                if deg[b]:
+                    infos[b][i]["degenerate"] = int(deg[b])
         return infos
 
     # ------------------------------------------------------------------- API
@@ -168,7 +177,16 @@ class MultiAgentConstrainEnv(MultiAgentEnv):
 
 
 class MultiAgentGraphConstrainEnv(MultiAgentConstrainEnv):
+    """node_obs="absolute" (default): every agent receives the env's node
+    table; node_obs="ego": agent i receives it relative to itself
+    (InforMARL-style, gsmarl_amd.ego), derived on the device per call."""
     with_graph = True
+
+    def __init__(self, cfg: Optional[EnvConfig] = None, device="cuda", node_obs: str = "absolute", **kw):
+        if node_obs not in ("absolute", "ego"):
+            raise ValueError("node_obs must be 'absolute' or 'ego'")
+        super().__init__(cfg, device, **kw)
+        self.node_obs = node_obs
 
     def _dense_adj(self, out) -> np.ndarray:
         """InforMARL-style adjacency: adj[b, s, d] = distance of edge s->d, else 0."""
@@ -179,13 +197,20 @@ class MultiAgentGraphConstrainEnv(MultiAgentConstrainEnv):
         return adj.view(B, E, E).cpu().numpy()
 
     def _graph_obs(self, out):
-        node = out["node_feat"].cpu().numpy()
         adj = self._dense_adj(out)
         aid = out["agent_id"].cpu().numpy()[..., None]
+        B, N = self.num_envs, self.n
+        if self.node_obs == "ego":
+            from .ego import EgoView
+            node = EgoView(out["node_feat"], N).all().cpu().numpy()            # [B, N, E, 7]
+            if self.num_envs == 1:
+                n = self.n_active
+                return ([aid[0, i] for i in range(n)], [node[0, i] for i in range(n)], [adj[0]] * n)
+            return (aid, node, np.repeat(adj[:, None], N, axis=1))
+        node = out["node_feat"].cpu().numpy()
         if self.num_envs == 1:
             n = self.n_active
             return ([aid[0, i] for i in range(n)], [node[0]] * n, [adj[0]] * n)
-        B, N = self.num_envs, self.n
         return (aid, np.repeat(node[:, None], N, axis=1), np.repeat(adj[:, None], N, axis=1))
 
     def reset(self, seed: Optional[int] = None):

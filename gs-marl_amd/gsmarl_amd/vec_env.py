@@ -20,6 +20,8 @@ obs [B,N,6], agent_id [B,N,1], node_obs [B,N,E,7], adj [B,N,E,E],
 rewards / costs [B,N,1], dones [B,N] (bool). Episode ends reset in-kernel and
 the returned observation is the new episode's, as the MAPPO worker does.
 
+``node_obs="ego"`` gives each agent the node table relative to itself
+(InforMARL-style, gsmarl_amd.ego) instead of the shared absolute table.
 ``output="torch"`` keeps everything on the device (no host copies; node_obs /
 adj become expand() views, not copies); ``output="numpy"`` returns host arrays
 like the subprocess vec-env. ``graph="dense"`` builds the InforMARL dense
@@ -42,11 +44,15 @@ from .spaces import Box, Discrete
 class GpuGraphVecEnv:
     """``GraphSubprocVecEnv`` / ``GraphDummyVecEnv`` replacement on one GPU."""
 
-    def __init__(self, cfg: EnvConfig, device="cuda", output: str = "numpy", graph: str = "dense"):
+    def __init__(self, cfg: EnvConfig, device="cuda", output: str = "numpy", graph: str = "dense",
+                 node_obs: str = "absolute"):
         if output not in ("numpy", "torch"):
             raise ValueError("output must be 'numpy' or 'torch'")
         if graph not in ("dense", "coo"):
             raise ValueError("graph must be 'dense' or 'coo'")
+        if node_obs not in ("absolute", "ego"):
+            raise ValueError("node_obs must be 'absolute' or 'ego'")
+        self.node_obs = node_obs
         self.cfg = cfg
         self.output = output
         self.graph_mode = graph
@@ -93,7 +99,11 @@ class GpuGraphVecEnv:
 
     def _graph_obs(self, out):
         B, N = self.num_envs, self.num_agents
-        node = out["node_feat"].unsqueeze(1).expand(B, N, *out["node_feat"].shape[1:])
+        if self.node_obs == "ego":   # agent i's table relative to itself (gsmarl_amd.ego)
+            from .ego import EgoView
+            node = EgoView(out["node_feat"], N).all()
+        else:
+            node = out["node_feat"].unsqueeze(1).expand(B, N, *out["node_feat"].shape[1:])
         adj = None
         if self.graph_mode == "dense":
             a = self._dense_adj(out)
@@ -103,13 +113,18 @@ class GpuGraphVecEnv:
 
     def _infos(self, out):
         """Per env, per agent dicts with the agent's cost; finished envs also
-        carry the finished episode's totals (sum reward, sum cost)."""
+        carry the finished episode's totals (sum reward, sum cost), degenerate
+        envs their App. A S16 flags."""
         c = out["cost"].cpu().numpy()
         d = out["done"].cpu().numpy().astype(bool)
+        deg = out["degenerate"].cpu().numpy()
         last = self.batch.t["ep_last"].cpu().numpy() if d.any() else None
         infos = []
         for b in range(self.num_envs):
             row = [{"cost": float(c[b, i])} for i in range(self.num_agents)]
+            if deg[b]:   # App. A S16 flags (coincident colliders / non-finite agent)
+                for info in row:
+                    info["degenerate"] = int(deg[b])
             if d[b]:
                 for info in row:
                     info["episode"] = {"r": float(last[b, 0]), "c": float(last[b, 1])}

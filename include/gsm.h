@@ -32,8 +32,10 @@
 extern "C" {
 #endif
 
-/* 4: lagged-emission graph chains (GSM_GRAPH_UNFUSED / _LAG_ONLY), gsm_render */
-#define GSM_ABI_VERSION 4
+/* 4: lagged-emission graph chains (GSM_GRAPH_UNFUSED / _LAG_ONLY), gsm_render
+ * 5: degenerate-state handling: gsm_config.strict_degenerate,
+ *    gsm_buffers.degenerate */
+#define GSM_ABI_VERSION 5
 
 typedef enum gsm_status {
     GSM_OK = 0,
@@ -91,6 +93,13 @@ typedef struct gsm_config {
     /* ragged scenarios (ignored by navigation) */
     int32_t n_agents_min;     /* mixed: N_env drawn from [n_agents_min, n_agents] */
     float formation_radius;   /* polygon: N-gon radius (readme.md:89 -> 0.5)  */
+    /* App. A S16. A coincident collider pair (d = 0, at least one agent) has
+     * no direction: by default its contact force is guarded to zero; with
+     * strict_degenerate != 0 it is NaN as in MPE's get_collision_force
+     * (delta / dist with dist = 0), and, as MPE evaluates every pair, an
+     * agent whose position is NaN makes the force of every agent of its env
+     * NaN. Either way the env is flagged in gsm_buffers.degenerate. */
+    int32_t strict_degenerate;
 } gsm_config;
 
 /* Sizes the caller must allocate (gsm_query_sizes). */
@@ -133,7 +142,16 @@ typedef struct gsm_buffers {
     /* ragged scenarios only (may be NULL for navigation) */
     int32_t *env_shape;       /* [B]    N_env | scenario << 8 (set at every layout) */
     int32_t *assign;          /* [B][N] polygon/line slot of each agent (LSA), -1 else */
+    /* optional (NULL: not written): per env, after every reset/step/observe,
+     * GSM_DEGENERATE_COINCIDENT if two colliders (at least one an agent) sit
+     * at the same position — the next step meets d = 0 — and
+     * GSM_DEGENERATE_NONFINITE if an agent position is not finite (strict
+     * mode, or a caller-written state) */
+    uint8_t *degenerate;      /* [B] */
 } gsm_buffers;
+
+#define GSM_DEGENERATE_COINCIDENT 1
+#define GSM_DEGENERATE_NONFINITE 2
 
 /* Output redirection (an on-device rollout buffer
  * filled without copies). Where one step / observe writes its outputs; NULL

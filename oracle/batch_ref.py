@@ -50,6 +50,7 @@ DEFAULTS = dict(
     dt=0.1, damping=0.25, mass=1.0, contact_force=100.0, contact_margin=1e-3,
     sensitivity=5.0, max_speed=0.0, world_half=None,
     agent_size=0.05, goal_size=0.05, obstacle_size=0.08, sense_radius=0.5,
+    strict_degenerate=False,   # Appendix A S16: MPE's NaN for a coincident pair instead of the guard
 )
 
 
@@ -154,7 +155,11 @@ def physics(cfg, pos, vel, actions, fmt, dtype=np.float64):
 
     Only agents are movable; goals (non-colliding) and obstacles (immovable)
     keep their positions. A coincident pair (d == 0) contributes zero force
-    (Appendix A S16 guard; MPE itself would produce NaN).
+    (Appendix A S16 guard), as does a pair with a non-finite distance. With
+    ``cfg.strict_degenerate`` every pair is evaluated as MPE does: a coincident
+    pair's force is 0/0 = NaN, and a NaN agent position makes every pair it
+    is in NaN — hence every agent of its env, whose pair with it MPE always
+    evaluates.
     """
     sp = Spec(cfg, dtype)
     f = sp.dtype.type
@@ -167,15 +172,24 @@ def physics(cfg, pos, vel, actions, fmt, dtype=np.float64):
     dx, dy = delta[..., 0], delta[..., 1]
     d2 = dx * dx + dy * dy
     d = np.sqrt(d2)
-    valid = (d2 > 0) & ~np.eye(N, sp.M, dtype=bool)[None]
+    offdiag = ~np.eye(N, sp.M, dtype=bool)[None]
+    strict = bool(getattr(cfg, "strict_degenerate", False))
+    valid = offdiag if strict else (d2 > 0) & offdiag
     dsafe = np.where(valid, d, f(1))
-    with np.errstate(over="ignore"):
+    with np.errstate(over="ignore", invalid="ignore", divide="ignore"):
         pen = np.logaddexp(f(0), -(dsafe - sp.dmin[None, None, :]) / sp.k) * sp.k
-    fx = np.where(valid, sp.cf * dx / dsafe * pen, f(0))
-    fy = np.where(valid, sp.cf * dy / dsafe * pen, f(0))
+        fx = np.where(valid, sp.cf * dx / dsafe * pen, f(0))
+        fy = np.where(valid, sp.cf * dy / dsafe * pen, f(0))
+    if strict:
+        # a NaN agent j also reaches agent i through the pair (j, i) that MPE
+        # evaluates from j's side; the [B,N,M] sum above covers (i, j) only
+        bad_env = ~np.isfinite(pa).all(axis=(1, 2))
+        fx[bad_env] = np.nan
+        fy[bad_env] = np.nan
     F = action_force(cfg, actions, fmt, dtype) + np.stack([fx.sum(-1), fy.sum(-1)], axis=-1)
     v = vel * sp.omd
-    v = v + (F / sp.mass) * sp.dt
+    with np.errstate(invalid="ignore"):
+        v = v + (F / sp.mass) * sp.dt
     if sp.max_speed > 0:
         s = np.sqrt(v[..., 0] * v[..., 0] + v[..., 1] * v[..., 1])
         over = s > sp.max_speed
@@ -284,12 +298,27 @@ def new_state(cfg, seed=None, dtype=np.float32):
     )
 
 
+def degenerate(cfg, pos):
+    """Appendix A S16 flags per env (uint8 [B]): 1 = two colliders, at least
+    one an agent, at the same position (fp32 d2 = 0: the next step meets
+    d = 0); 2 = an agent position is not finite."""
+    sp = Spec(cfg, np.float32)
+    N = sp.N
+    pos = np.asarray(pos, dtype=np.float32)
+    pa, pc = pos[:, :N], pos[:, sp.cidx]
+    with np.errstate(invalid="ignore", over="ignore"):
+        d2 = _pair_d2(pa[:, :, None, :], pc[:, None, :, :])       # [B,N,M] fp32
+    coinc = ((d2 == 0) & ~np.eye(N, sp.M, dtype=bool)[None]).any(axis=(1, 2))
+    nonfin = ~np.isfinite(pa).all(axis=(1, 2))
+    return (coinc.astype(np.uint8) | (nonfin.astype(np.uint8) << 1)).astype(np.uint8)
+
+
 def observe(cfg, st, dtype):
     pos, vel = st["pos"], st["vel"]
     r, c = reward_cost(cfg, pos, dtype)
     ptr, ei, attr = edges(cfg, pos, dtype)
     return dict(reward=r, cost=c, node_feat=node_features(cfg, pos, vel, dtype),
-                edge_ptr=ptr, edge_index=ei, edge_attr=attr)
+                edge_ptr=ptr, edge_index=ei, edge_attr=attr, degenerate=degenerate(cfg, pos))
 
 
 def step(cfg, st, actions, fmt=1, dtype=np.float64, seed=None):

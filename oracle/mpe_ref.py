@@ -76,6 +76,7 @@ class World:
         self.damping = 0.25
         self.contact_force = 1e2
         self.contact_margin = 1e-3
+        self.strict = False   # Appendix A S16: True = MPE's unguarded 0/0 force
 
     @property
     def entities(self):
@@ -111,12 +112,13 @@ class World:
             return None, None
         delta = ea.state.p_pos - eb.state.p_pos
         dist = np.sqrt(np.sum(np.square(delta)))
-        if dist == 0.0:            # Appendix A S16 guard (MPE would divide by 0)
+        if not self.strict and not dist > 0.0:   # Appendix A S16 guard (MPE divides by 0)
             return None, None
         dist_min = ea.size + eb.size
         k = self.contact_margin
-        penetration = np.logaddexp(0, -(dist - dist_min) / k) * k
-        force = self.contact_force * delta / dist * penetration
+        with np.errstate(invalid="ignore", divide="ignore"):
+            penetration = np.logaddexp(0, -(dist - dist_min) / k) * k
+            force = self.contact_force * delta / dist * penetration
         return (+force if ea.movable else None), (-force if eb.movable else None)
 
     def integrate_state(self, p_force):
@@ -140,6 +142,7 @@ class NavigationScenario:
         w = World()
         w.dt, w.damping = cfg.dt, cfg.damping
         w.contact_force, w.contact_margin = cfg.contact_force, cfg.contact_margin
+        w.strict = bool(getattr(cfg, "strict_degenerate", False))
         self.cfg = cfg
         for i in range(cfg.n_agents):
             a = Agent()

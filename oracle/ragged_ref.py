@@ -167,6 +167,10 @@ def assignment(cfg, scn, n, pos_c):
     dx = pa[:, None, 0] - s[None, :, 0]
     dy = pa[:, None, 1] - s[None, :, 1]
     C = np.sqrt(dx * dx + dy * dy).astype(np.float32)
+    if not np.isfinite(pa).all():
+        # Appendix A S16 (strict mode / caller-written NaN state): scipy raises
+        # on such a matrix; the contract is no assignment (-1) and a NaN cost
+        return np.full(n, -1, np.int64), C
     return linear_sum_assignment(C.astype(np.float64)), C
 
 
@@ -208,7 +212,9 @@ def reward_cost_env(cfg, scn, n, pos_c, dtype):
         r, sigma = r[0], None
     else:
         sigma, C = assignment(cfg, scn, n, np.asarray(pos_c, np.float32))
-        if np.dtype(dtype) == np.float64:
+        if (sigma < 0).any():
+            r = np.full(n, np.nan, dtype)
+        elif np.dtype(dtype) == np.float64:
             s = slots(cfg, scn, n, np.asarray(pos_c, np.float32)[n:]).astype(np.float64)
             d = np.asarray(pos_c, np.float64)[:n] - s[sigma]
             r = -np.sqrt(d[:, 0] * d[:, 0] + d[:, 1] * d[:, 1])
@@ -230,7 +236,7 @@ def node_features_env(cfg, rs, scn, n, pos_c, vel, sigma):
     nf[idx, 2:4] = pos_c
     nf[idx, 6] = types
     nf[:n, 0:2] = vel
-    tgt = pos_c[n:2 * n] if scn == SCN_NAV else slots(cfg, scn, n, pos_c[n:n + T])[sigma]
+    tgt = pos_c[n:2 * n] if scn == SCN_NAV else slots(cfg, scn, n, pos_c[n:n + T])[np.maximum(sigma, 0)]
     nf[:n, 4:6] = tgt - pos_c[:n]
     return nf
 
@@ -257,6 +263,21 @@ def adjacency_env(cfg, scn, n, pos_c):
             conn[i, n + t] = True
             conn[n + t, i] = True
     return conn, d2
+
+
+def degenerate_env(scn, n, pos_c):
+    """Appendix A S16 flags of one env (as batch_ref.degenerate): 1 = two
+    colliders, at least one an agent, at fp32 d2 = 0; 2 = a non-finite agent."""
+    pos_c = np.asarray(pos_c, np.float32)
+    T, O = n_targets(scn, n), n_obstacles(scn, n)
+    coll = np.concatenate([pos_c[:n], pos_c[n + T:n + T + O]])
+    with np.errstate(invalid="ignore", over="ignore"):
+        dx = coll[:n, None, 0] - coll[None, :, 0]
+        dy = coll[:n, None, 1] - coll[None, :, 1]
+        d2 = dx * dx + dy * dy
+    coinc = bool(((d2 == 0) & ~np.eye(n, n + O, dtype=bool)).any())
+    nonfin = not np.isfinite(pos_c[:n]).all()
+    return np.uint8(int(coinc) | (int(nonfin) << 1))
 
 
 def edges_env(cfg, rs, scn, n, pos_c, b):
@@ -298,10 +319,12 @@ def observe(cfg, st, dtype=np.float32):
     B = st["pos"].shape[0]
     nf = np.zeros((B, rs.Emax, br.NODE_FEAT_DIM), np.float32)
     assign = np.full((B, rs.Nmax), -1, np.int32)
+    deg = np.zeros(B, np.uint8)
     src, dst, attr, counts = [], [], [], np.zeros(B, np.int64)
     for b in range(B):
         n, scn, pc = _compact(rs, st, b)
         pc32 = np.asarray(pc, np.float32)
+        deg[b] = degenerate_env(scn, n, pc32)
         sigma = None
         if scn != SCN_NAV:
             sigma, _ = assignment(cfg, scn, n, pc32)
@@ -316,7 +339,7 @@ def observe(cfg, st, dtype=np.float32):
     np.cumsum(counts, out=ptr[1:])
     ei = np.stack([np.concatenate(src), np.concatenate(dst)]).astype(np.int32) if B else np.zeros((2, 0), np.int32)
     return dict(node_feat=nf, assign=assign, edge_ptr=ptr, edge_index=ei,
-                edge_attr=np.concatenate(attr) if B else np.zeros(0, np.float32))
+                edge_attr=np.concatenate(attr) if B else np.zeros(0, np.float32), degenerate=deg)
 
 
 def step(cfg, st, actions, fmt=1, dtype=np.float64):

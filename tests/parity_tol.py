@@ -38,6 +38,10 @@ def check_state(got, ref, what):
     """|got - ref| <= state_tol(ref) elementwise; records the max error."""
     got = np.asarray(got, dtype=np.float64)
     ref = np.asarray(ref, dtype=np.float64)
+    # NaN where MPE gives NaN (App. A S16 strict mode) and nowhere else
+    gn, rn = np.isnan(got), np.isnan(ref)
+    assert np.array_equal(gn, rn), f"{what}: NaN pattern differs at {np.argwhere(gn != rn)[:5].tolist()}"
+    got, ref = np.where(gn, 0.0, got), np.where(rn, 0.0, ref)
     err = np.abs(got - ref)
     m = float(err.max()) if err.size else 0.0
     record(what, m)

@@ -80,3 +80,30 @@ def test_eval_env_ids_follow_training_envs():
     ev = make_eval_env(_args(), device=DEV)
     assert ev.num_envs == 2 and ev.cfg.env_base == 16 and ev.cfg.seed == 3 * 50000
     ev.close()
+
+
+def test_ego_node_obs():
+    """node_obs="ego" (InforMARL-style per-agent view, gsmarl_amd.ego): agent
+    i's table is the absolute table relative to agent i, in the vec-env and in
+    the single-env drop-in class."""
+    from gsmarl_amd import EnvConfig, GpuGraphVecEnv, MultiAgentGraphConstrainEnv
+    from gsmarl_amd.ego import EgoView
+    cfg = dict(n_agents=5, n_envs=8, seed=4)
+    vec = GpuGraphVecEnv(EnvConfig(**cfg), DEV, output="torch", node_obs="ego")
+    vec.reset(seed=4)
+    a = torch.randint(0, 5, (8, 5), dtype=torch.int32, device=DEV)
+    obs, aid, node, adj, rew, cost, done, _ = vec.step(a)
+    nf = vec.batch.t["node_feat"]
+    assert node.shape == (8, 5, nf.shape[1], 7)
+    assert torch.equal(node, EgoView(nf, 5).all())
+    for i in range(5):
+        assert torch.all(node[:, i, i, 0:4] == 0)
+        assert torch.allclose(node[:, i, :, 2:4], nf[:, :, 2:4] - nf[:, i:i + 1, 2:4])
+    vec.close()
+    env = MultiAgentGraphConstrainEnv(EnvConfig(n_agents=4, n_envs=1, seed=2), DEV, node_obs="ego")
+    obs_n, aid_n, node_n, adj_n = env.reset(seed=2)
+    nf = env.batch.t["node_feat"]
+    assert len(node_n) == 4
+    for i in range(4):
+        assert np.array_equal(node_n[i], EgoView(nf, 4)[i][0].cpu().numpy())
+    env.close()

@@ -73,6 +73,56 @@ def test_coincident_guard():
     assert cost[0].tolist() == [1.0, 1.0]          # coincident agents collide
 
 
+def test_coincident_strict_is_mpe_nan_and_spreads():
+    """Appendix A S16 strict mode: MPE's delta/dist = 0/0 makes both agents of
+    a coincident pair NaN; on the next step every pair with a NaN agent is NaN,
+    so every agent of the env is; other envs are untouched. The flags follow."""
+    cfg = br.make_cfg(n_agents=3, n_obstacles=1, strict_degenerate=True, n_envs=2)
+    base = [[0.5, 0.5], [0.5, 0.5], [-1.0, -1.0], [1, 1], [2, 2], [0, 2], [1.5, -1.5]]
+    pos = np.array([base, base], np.float64)
+    pos[1, 1] = [0.9, 0.5]                              # env 1: no coincident pair
+    vel = np.zeros((2, 3, 2))
+    assert br.degenerate(cfg, pos).tolist() == [1, 0]
+    p, v = br.physics(cfg, pos, vel, np.zeros((2, 3), int), 1)
+    assert np.isnan(v[0, :2]).all() and np.isnan(p[0, :2]).all()
+    assert np.isfinite(v[0, 2]).all() and np.isfinite(p[0, 2]).all() and np.isfinite(p[1]).all()
+    assert br.degenerate(cfg, p).tolist() == [2, 0]
+    p2, v2 = br.physics(cfg, p, v, np.zeros((2, 3), int), 1)
+    assert np.isnan(v2[0]).all() and np.isfinite(v2[1]).all()
+    assert np.array_equal(p2[0, 3:], pos[0, 3:])        # landmarks never move
+    # the guard (default): zero contact force for the coincident pair, finite
+    gcfg = br.make_cfg(n_agents=3, n_obstacles=1, n_envs=2)
+    pg, vg = br.physics(gcfg, pos, vel, np.zeros((2, 3), int), 1)
+    assert np.isfinite(pg).all() and np.all(vg[0, :2] == 0)
+    # an agent on an obstacle is flagged too; an obstacle pair alone is not
+    q = np.array([base], np.float64)
+    q[0, 1] = [0.2, 0.2]
+    q[0, 2] = q[0, 6]
+    assert br.degenerate(gcfg, q).tolist() == [1]
+
+
+def test_strict_mpe_ref_equals_batch_ref():
+    cfg = br.make_cfg(n_agents=4, n_obstacles=2, strict_degenerate=True)
+    env = mr.GraphConstrainEnv(cfg)
+    env.reset(seed=1)
+    pos = _crowd(4, 2, 0.3, 4)
+    pos[3] = pos[8]                                     # agent 3 on obstacle 0
+    vel = np.zeros((4, 2))
+    env.set_state(pos, vel)
+    st = dict(pos=pos[None].copy(), vel=vel[None].copy(), step=np.zeros(1, np.int32),
+              episode=np.zeros(1, np.int32), ep_acc=np.zeros((1, 2)), ep_last=np.zeros((1, 2)))
+    for t in range(3):
+        a = np.array([1, 2, 3, 4])
+        with np.errstate(invalid="ignore"):
+            env.step(list(np.eye(5)[a]))
+        st, ob = br.step(cfg, st, a[None], 1, np.float64)
+        p, v = env.get_state()
+        assert np.array_equal(np.isnan(p), np.isnan(st["pos"][0])), t
+        assert np.allclose(p, st["pos"][0], rtol=0, atol=1e-12, equal_nan=True)
+        assert np.allclose(v, st["vel"][0], rtol=0, atol=1e-12, equal_nan=True)
+    assert np.isnan(p[:4]).all()                        # spread to every agent by step 2
+
+
 @pytest.mark.parametrize("k,u", [(0, (0, 0)), (1, (5, 0)), (2, (-5, 0)), (3, (0, 5)), (4, (0, -5)), (7, (0, 0))])
 def test_action_mapping(k, u):
     cfg = br.make_cfg(n_agents=1)
