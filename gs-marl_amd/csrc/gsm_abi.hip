@@ -434,6 +434,9 @@ int gsm_bind(gsm_handle *h, const gsm_buffers *b) {
     p.env_shape = b->env_shape;
     p.assign = b->assign;
     p.degenerate = b->degenerate;
+    p.lsa_v = (b->lsa_v && b->lsa_col) ? b->lsa_v : nullptr;
+    p.lsa_col = p.lsa_v ? b->lsa_col : nullptr;
+    p.lsa_stats = b->lsa_stats;
     h->bound = true;
     drop_graph(h);   // a captured graph holds the old pointers
     return GSM_OK;

@@ -58,6 +58,9 @@ struct DevParams {
     int32_t *env_shape;       // [B] ragged: N_env | scenario << 8
     int32_t *assign;          // [B][N] ragged: LSA slot per agent
     uint8_t *degenerate;      // [B] optional: GSM_DEGENERATE_* bits of the launch's final state
+    double *lsa_v;            // [B][N] optional: ragged assignment warm start (column duals)
+    int32_t *lsa_col;         // [B][N] with lsa_v: the last matching (row -> column)
+    int32_t *lsa_stats;       // [B][2] optional: certified warm starts, assignments solved
     const int32_t *block_order;   // ragged mixed: workgroup -> env block, heaviest first (nullptr: identity)
     int64_t edge_capacity;
     const void *actions;

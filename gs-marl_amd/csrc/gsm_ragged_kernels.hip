@@ -156,12 +156,38 @@ __device__ __forceinline__ float2 slot_of(const DevParams &p, const RShape &s, i
     return make_float2(l0.x + ex * tj, l0.y + ey * tj);
 }
 
-// Square linear sum assignment of N <= 32 agents (rows) to N slots (columns),
-// scipy's rectangular_lsap recurrence (oracle/lsa_ref.py) with lane k holding
-// row k and column k. C[i][j] = |p_i - slot_j| in fp32 (staged in LDS),
-// all dual arithmetic in float64 in scipy's operation order. Returns the
-// lane's column (row `lane`), and its cost in *own.
-__device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, float *own, int *iters = nullptr) {
+// Per-env warm-start state of the assignment (optional caller buffers,
+// gsm_buffers.lsa_v / lsa_col / lsa_stats): the column duals and the matching
+// of the env's last assignment, and (hits, solves) counters.
+struct LsaWarm {
+    double *v;        // [N_max] column duals
+    int32_t *col;     // [N_max] column of each row (-1: none)
+    int32_t *stats;   // [2] certified warm starts, assignments solved
+};
+
+// Square linear sum assignment of N <= 32 agents (rows) to N slots (columns)
+// with lane k holding row k and column k. C[i][j] = |p_i - slot_j| in fp32
+// (staged in LDS), all dual arithmetic in float64. Returns the lane's column
+// (row `lane`), and its cost in *own. The result is scipy's
+// linear_sum_assignment(C), ties included:
+//
+//  * warm start (w.v != nullptr): the previous step's column duals v and
+//    matching. Row duals u_i = min_j (C[i][j] - v_j) make every reduced cost
+//    r_ij = C[i][j] - u_i - v_j >= 0; each row keeps its previous column when
+//    that column attains its minimum (r = 0); the other rows are matched by
+//    scipy's augmenting step (below) from this feasible partial state. The
+//    result is accepted only with a certificate that it is the UNIQUE optimum:
+//    r >= -1e-11 everywhere and |r| <= 1e-11 on the matching, and no
+//    alternating cycle among the tight pairs (r <= 1e-9). Any other
+//    assignment differs from this one by cycles, each using a pair with
+//    r > 1e-9, so it costs at least 1e-9 - N * 1e-11 more (float64 rounding
+//    here and in scipy is ~1e-14), and scipy, which returns an optimum,
+//    returns this one. Without the certificate (ties, or a state the warm
+//    start cannot use):
+//  * cold: scipy's rectangular_lsap recurrence from scratch (oracle/lsa_ref.py),
+//    rows in order, with its tie rules.
+__device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, float *own, LsaWarm w,
+                        int *iters = nullptr) {
     const bool col = lane < N;
     // a non-finite agent position (strict mode, App. A S16; or a caller-written
     // state) has no assignment (scipy raises on such a cost matrix): slot -1,
@@ -194,7 +220,11 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
     double u = 0.0, v = 0.0;
     int col4row = -1, row4col = -1;
     const uint64_t colmask = N >= 64 ? ~0ull : ((1ull << N) - 1);
-    for (int cur = 0; cur < N; ++cur) {
+
+    // scipy's augmenting step for row `cur` from the current duals and
+    // matching: shortest augmenting path, dual update, augmentation. Returns
+    // false if no free column was reached (never for finite costs).
+    auto augment = [&](int cur) -> bool {
         double spc = kInf;
         int path = -1;
         int rpos = N - 1 - lane;     // position in scipy's `remaining` list (filled in reverse)
@@ -261,7 +291,7 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
             }
             i = r4c;
         }
-        if (sink < 0) break;   // unreachable for finite costs
+        if (sink < 0) return false;   // unreachable for finite costs
         const bool SR = (srm >> lane) & 1, SC = ((colmask & ~remm) >> lane) & 1;
         // dual update (before augmenting: col4row is the previous matching)
         const double spc_c = __shfl(spc, col4row < 0 ? 0 : col4row);
@@ -278,6 +308,91 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
             j = nj;
             if (pi_ == cur) break;
         }
+        return true;
+    };
+
+    // uniqueness certificate of the current matching and duals: dual
+    // feasibility and complementary slackness (to rounding), then no
+    // alternating cycle of tight pairs (r <= 1e-9) — the graph with an arc
+    // from row i to the row holding column j for every tight unmatched (i, j)
+    // is acyclic (peeled sink by sink)
+    auto certified = [&]() -> bool {
+        bool good = true;
+        uint32_t tight = 0;   // lane i: tight unmatched columns of row i
+        for (int i = 0; i < N; ++i) {
+            const double ui = rl_d(u, i);
+            const int ci = __builtin_amdgcn_readlane(col4row, i);
+            const double r = (double)ccol[i] - ui - v;
+            good &= !col || (lane == ci ? fabs(r) <= 1e-11 : r >= -1e-11);
+            const uint64_t t = __builtin_amdgcn_ballot_w64(col && lane != ci && r <= 1e-9);
+            tight = writelane_u32((uint32_t)t, (uint32_t)i, tight);
+        }
+        if (!__all(good)) return false;
+        uint64_t rows = colmask, cols = colmask;   // rows not yet peeled, their columns
+        for (int it = 0; it < N && rows; ++it) {
+            const bool sink = ((rows >> lane) & 1) && !(tight & (uint32_t)cols);
+            const uint64_t S = __builtin_amdgcn_ballot_w64(sink);
+            if (!S) break;                       // every remaining row is on a cycle
+            rows &= ~S;
+            cols &= ~__builtin_amdgcn_ballot_w64(col && row4col >= 0 && ((S >> row4col) & 1));
+        }
+        return rows == 0;
+    };
+
+    bool solved = false;
+    if (w.v) {
+        const double v0 = col ? w.v[lane] : 0.0;
+        const int c0 = col ? w.col[lane] : -1;
+        if (__all(!col || __builtin_isfinite(v0))) {
+            // feasible row duals from the previous v; rows whose previous
+            // column still attains their minimum keep it, the others are
+            // re-matched by scipy's augmenting step. (Keeping the whole
+            // previous matching and restoring feasibility by Bellman-Ford on
+            // v certified only 5% of N = 24 polygon steps under random
+            // actions — the optimum moves — and cost more than it saved.)
+            v = v0;
+            uint64_t taken = 0, freerows = 0;
+            for (int i = 0; i < N; ++i) {
+                const double r = col ? (double)ccol[i] - v : kInf;
+                const int key = col ? f32_order_key((float)r + 0.0f) : 0x7fffffff;
+                const int kmin = min32_i(key);
+                const uint64_t near = __builtin_amdgcn_ballot_w64(key == kmin) & colmask;
+                const double m = !(near & (near - 1)) ? rl_d(r, first_lane(near))
+                                                      : min32((near >> lane) & 1 ? r : kInf);
+                if (lane == i) u = m;
+                const int ci = __builtin_amdgcn_readlane(c0, i);
+                const bool keep = ci >= 0 && ci < N && !((taken >> ci) & 1) && rl_d(r, ci) == m;
+                if (keep) {
+                    taken |= 1ull << ci;
+                    if (lane == i) col4row = ci;
+                    if (lane == ci) row4col = i;
+                } else {
+                    freerows |= 1ull << i;
+                }
+            }
+#ifdef GSM_STAMPS   // diagnostic builds: rows the warm start re-augments (high half)
+            if (iters) *iters += __popcll(freerows) << 16;
+#endif
+            bool ok = true;
+            for (uint64_t fr = freerows; fr && ok; fr &= fr - 1) ok = augment(first_lane(fr));
+            solved = ok && certified();
+        }
+        if (w.stats && lane == 0) {
+            w.stats[0] += solved ? 1 : 0;
+            w.stats[1] += 1;
+        }
+    }
+    if (!solved) {
+        u = 0.0;
+        v = 0.0;
+        col4row = -1;
+        row4col = -1;
+        for (int cur = 0; cur < N; ++cur)
+            if (!augment(cur)) break;
+    }
+    if (w.v && col) {
+        w.v[lane] = v;
+        w.col[lane] = col4row;
     }
     *own = col && col4row >= 0 ? s_cost[lane * N + col4row] : 0.0f;
     return col ? col4row : -1;
@@ -293,6 +408,8 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
     float2 *s_pos = (float2 *)(lds + 4 * Nmax * Nmax);          // [E] staged rows
     float2 *pos_b = p.pos + eb * Emax;
     const bool do_reset = p.mode == kModeReset && (p.env_mask == nullptr || p.env_mask[b] != 0);
+    const LsaWarm lsa_warm{p.lsa_v ? p.lsa_v + eb * Nmax : nullptr, p.lsa_col ? p.lsa_col + eb * Nmax : nullptr,
+                           p.lsa_stats ? p.lsa_stats + 2 * eb : nullptr};
     int t = p.step_count[b];
     int ep = p.episode[b];
     float2 acc = p.ep_acc[b];
@@ -411,7 +528,7 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
         float own;
         int nit = 0;
         GSM_STAMP(p, b, 0);
-        sigma = wave_lsa(s.N, lane, cp, slot, s_cost, &own, &nit);
+        sigma = wave_lsa(s.N, lane, cp, slot, s_cost, &own, lsa_warm, &nit);
         GSM_STAMP(p, b, 1);
 #ifdef GSM_STAMPS
         if (p.stamps && lane == 0) p.stamps[(int64_t)b * 16 + 2] = (uint64_t)nit;
@@ -440,7 +557,7 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
             if (s.scn != kScnNav) {
                 slot = slot_of(p, s, lane, tp);
                 float own;
-                sigma = wave_lsa(s.N, lane, cp, slot, s_cost, &own);
+                sigma = wave_lsa(s.N, lane, cp, slot, s_cost, &own, lsa_warm);
             }
         }
     }

@@ -49,7 +49,8 @@ class GsmSizes(C.Structure):
 
 BUFFER_FIELDS = ["pos", "vel", "step_count", "episode", "ep_acc", "ep_last", "node_feat",
                  "reward", "cost", "done", "edge_count", "block_edge_sum", "edge_ptr",
-                 "edge_index", "edge_attr", "row_mask", "contact_mask", "env_shape", "assign", "degenerate"]
+                 "edge_index", "edge_attr", "row_mask", "contact_mask", "env_shape", "assign", "degenerate",
+                 "lsa_v", "lsa_col", "lsa_stats"]
 
 
 class GsmBuffers(C.Structure):

@@ -76,8 +76,15 @@ class GpuBatchEnv:
             assign=torch.full((B, N), -1, dtype=i32, device=dev),
             # App. A S16 flags per env (GSM_DEGENERATE_*: 1 coincident pair, 2 non-finite agent)
             degenerate=torch.zeros(B, dtype=torch.uint8, device=dev),
+            # ragged assignment warm start (column duals, matching) and its counters
+            lsa_v=torch.zeros(B, N, dtype=torch.float64, device=dev),
+            lsa_col=torch.full((B, N), -1, dtype=i32, device=dev),
+            lsa_stats=torch.zeros(B, 2, dtype=i32, device=dev),
         )
-        bufs = _lib.GsmBuffers(**{k: self.t[k].data_ptr() for k in _lib.BUFFER_FIELDS})
+        ptrs = {k: self.t[k].data_ptr() for k in _lib.BUFFER_FIELDS}
+        if not cfg.lsa_warm_start:   # every assignment solved from scratch
+            ptrs["lsa_v"] = ptrs["lsa_col"] = None
+        bufs = _lib.GsmBuffers(**ptrs)
         _lib.check(self.lib, self.lib.gsm_bind(self._h, C.byref(bufs)), self._h, "gsm_bind")
         self.agent_id = torch.arange(N, dtype=torch.int64, device=dev).expand(B, N)
         self._graph_actions = {}
@@ -270,6 +277,12 @@ class GpuBatchEnv:
         self._chk(self.lib.gsm_graph_kernel_ms(self._h, int(slot), C.byref(a), C.byref(b), C.byref(c)),
                   "gsm_graph_kernel_ms")
         return a.value, b.value, c.value
+
+    def lsa_warm_stats(self) -> tuple:
+        """(certified warm starts, assignments solved) since construction,
+        over the polygon/line envs of a ragged batch."""
+        s = self.t["lsa_stats"].to(torch.int64).sum(0)
+        return int(s[0].item()), int(s[1].item())
 
     # ---------------------------------------------------------------- metrics
     def episode_metrics(self) -> torch.Tensor:

@@ -39,6 +39,7 @@ class EnvConfig:
     n_agents_min: int = 3                  # mixed: N_env drawn from [n_agents_min, n_agents]
     formation_radius: float = 0.5          # polygon N-gon radius (readme.md:89)
     strict_degenerate: bool = False        # App. A S16: MPE's NaN for d = 0 pairs instead of the guard
+    lsa_warm_start: bool = True            # polygon/line: certified warm-started assignment (gsm.h lsa_v)
 
     def __post_init__(self):
         if self.scenario not in SCENARIOS:

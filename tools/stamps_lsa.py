@@ -20,13 +20,18 @@ env = GpuBatchEnv(EnvConfig(scenario=scn, n_agents=N, n_envs=B, seed=3), "cuda:0
 st = torch.zeros(max(B, 2 * env.sizes.n_blocks * 4), 16, dtype=torch.int64, device="cuda:0")
 env.lib.gsm_debug_set_stamps(env._h, C.c_void_p(st.data_ptr()))
 env.reset(seed=3, sync_edges=False)
+for _ in range(int(os.environ.get("ABL_WARM", 5))):   # steps before the measured one (warm-start state)
+    env.step(torch.randint(0, 5, (B, N), dtype=torch.int32, device="cuda:0"))
 torch.cuda.synchronize()
 st.zero_()
 env.step(torch.randint(0, 5, (B, N), dtype=torch.int32, device="cuda:0"))
 torch.cuda.synchronize()
 s = st.cpu().numpy().astype(np.int64)[:B]
-cyc, it = s[:, 1] - s[:, 0], s[:, 2]
-ok = it > 0
+cyc, raw = s[:, 1] - s[:, 0], s[:, 2]
+it, free = raw & 0xFFFF, (raw >> 16) & 0xFF
+ok = cyc > 0
 print(json.dumps(dict(scenario=scn, N=N, B=B, envs=int(ok.sum()), lsa_cycles_median=float(np.median(cyc[ok])),
+                      lsa_cycles_max=int(cyc[ok].max()),
                       iters_median=float(np.median(it[ok])), iters_max=int(it[ok].max()),
-                      cycles_per_iter_median=float(np.median(cyc[ok] / it[ok])))))
+                      free_rows_median=float(np.median(free[ok])), free_rows_max=int(free[ok].max()),
+                      warm_stats=env.lsa_warm_stats())))
