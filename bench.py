@@ -524,7 +524,7 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL):
     import torch
     L = args.kernel_launches
     seg = (N + cfg.n_obstacles) <= 64 and not cfg.ragged
-    lag = seg and not args.unfused
+    lag = seg and not args.unfused   # segmented chains: lagged emission
     env.capture(actions, L, slot=3, kernels="lag" if lag else "step", time_ends=True)
     env.replay(3)
     torch.cuda.synchronize()

@@ -260,7 +260,8 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
         const int sym = 16 * ((N + 1) / 2) + 16 * N * p->W + 8 * No * p->W + 16;
         p->tile_sym = sym <= 32768;
         if (p->tile_sym) p->wave_lds_step += sym;
-        p->wave_lds_emit = align16(8 * p->E + 4 * (gsm::kTileBlock / gsm::kWave));
+        // emit: positions, reductions and the staged edge words (gsm::kTileEmitScr)
+        p->wave_lds_emit = align16(8 * p->E + 4 * (gsm::kTileBlock / gsm::kWave) + 4 * gsm::kTileEmitScr);
     }
     const float L = c->world_half;
     p->L = L;

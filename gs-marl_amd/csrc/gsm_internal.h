@@ -14,6 +14,7 @@ enum : int32_t { kPathSeg = 1, kPathRagged = 2, kPathTile = 3 };
 #endif
 constexpr int kTileBlock = GSM_TILE_BLOCK;     // tile path: one workgroup per env
 enum : int32_t { kScnNav = 0, kScnPolygon = 1, kScnLine = 2, kScnMixed = 3 };
+constexpr int kTileEmitScr = 6144;   // tile emitter: staged edge words per env (24 KB of LDS)
 constexpr int kRaggedMaxAgents = 32;                                  // = GSM_RAGGED_MAX_AGENTS
 constexpr int kRaggedTable = kRaggedMaxAgents * (kRaggedMaxAgents + 1) / 2;   // rows n = 1..32
 #ifndef GSM_SEG_GMAX   // cap on envs per wave (C2, 3 x 4096: G = 4 runs 6.0 us per step against 6.9 at G = 10)

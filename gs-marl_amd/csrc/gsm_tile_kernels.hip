@@ -399,28 +399,79 @@ __device__ __forceinline__ int row_edges(const DevParams &p, const EdgeSink &out
     return n;
 }
 
+// Row r's edges in entity order as (source | destination << 16) entity-id
+// words at `at` (the staged form of row_edges<true>); returns the end.
+__device__ __forceinline__ uint32_t *expand_row(const DevParams &p, const uint64_t *rmask, int r, uint32_t *at) {
+    const int N = p.N, W = p.W;
+    const uint32_t src = (uint32_t)r;
+    if (r >= N && r < 2 * N) {   // goal row: goal i -> agent i
+        *at = src | ((uint32_t)(r - N) << 16);
+        return at + 1;
+    }
+    const uint64_t *row = rmask + (int64_t)(r < N ? r : r - N) * W;
+    bool goal_done = r >= N;
+    for (int k = 0; k < W; ++k) {
+        for (uint64_t bits = row[k]; bits; bits &= bits - 1) {
+            const int c = 64 * k + __builtin_ctzll(bits);
+            if (!goal_done && c >= N) {   // own goal sits between agents and obstacles
+                *at++ = src | ((uint32_t)(N + r) << 16);
+                goal_done = true;
+            }
+            *at++ = src | ((uint32_t)collider_entity(c, N) << 16);
+        }
+    }
+    if (!goal_done) *at++ = src | ((uint32_t)(N + r) << 16);
+    return at;
+}
+
 // Env b's edges at global offset `off` (workgroup-wide: barriers): each
 // thread takes a contiguous run of rows, counts them from the mask words, a
-// workgroup scan gives the run offsets, then the runs are written. s_red:
+// workgroup scan gives the run offsets. When the env's edges fit the LDS
+// scratch s_scr (scr_cap words) and the outputs, the runs are first expanded
+// into s_scr in CSR order and then written by every thread, edge e by thread
+// e mod 512 — coalesced stores and no row-length imbalance; otherwise each
+// thread writes its runs directly (bounded by the output capacity). s_red:
 // kTileWaves ints.
 __device__ __forceinline__ void emit_env(const DevParams &p, const EdgeSink &out, const float2 *s_pos,
-                                         const uint64_t *rmask, int64_t off, int *s_red) {
+                                         const uint64_t *rmask, int64_t off, int *s_red, uint32_t *s_scr,
+                                         int scr_cap, int32_t g0) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int E = p.E;
     const int R = (E + kTileBlock - 1) / kTileBlock;
     const int r0 = tid * R, r1 = min(E, r0 + R);
-    const int32_t g0 = (int32_t)((int64_t)blockIdx.x * E);
     int mine = 0;
     for (int r = r0; r < r1; ++r) mine += row_edges<false>(p, out, s_pos, rmask, r, 0, g0);
     const int incl = wave_scan(mine);
     __syncthreads();
     if (lane == 63) s_red[wave] = incl;
     __syncthreads();
-    int base = incl - mine;
-    for (int w = 0; w < wave; ++w) base += s_red[w];
-    int64_t o = off + base;
-    for (int r = r0; r < r1; ++r) o += row_edges<true>(p, out, s_pos, rmask, r, o, g0);
-    __syncthreads();   // s_red is reused by the caller
+    int base = incl - mine, total = 0;
+#pragma unroll
+    for (int w = 0; w < kTileWaves; ++w) {
+        const int t = s_red[w];
+        base += w < wave ? t : 0;
+        total += t;
+    }
+    if (total <= scr_cap && off + total <= out.cap) {   // workgroup-uniform
+        uint32_t *at = s_scr + base;
+        for (int r = r0; r < r1; ++r) at = expand_row(p, rmask, r, at);
+        __syncthreads();
+        int32_t *src = out.index + off, *dst = out.index + out.cap + off;
+        float *attr = out.attr + off;
+        for (int e = tid; e < total; e += kTileBlock) {
+            const uint32_t w = s_scr[e];
+            const uint32_t a = w & 0xffffu, b = w >> 16;
+            const float2 pa = s_pos[a], pb = s_pos[b];
+            const float dx = pa.x - pb.x, dy = pa.y - pb.y;
+            src[e] = g0 + (int32_t)a;
+            dst[e] = g0 + (int32_t)b;
+            attr[e] = sqrtf(dx * dx + dy * dy);
+        }
+    } else {
+        int64_t o = off + base;
+        for (int r = r0; r < r1; ++r) o += row_edges<true>(p, out, s_pos, rmask, r, o, g0);
+    }
+    __syncthreads();   // s_red and s_scr are reused by the caller
 }
 
 __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel(DevParams p) {
@@ -646,6 +697,8 @@ __global__ __launch_bounds__(kTileBlock) void gsm_emit_tile_kernel(DevParams p) 
     const int E = p.E;
     float2 *s_pos = (float2 *)smem;
     int *s_red = (int *)(s_pos + E);          // [kTileWaves]
+    uint32_t *s_scr = (uint32_t *)(s_red + kTileWaves);   // staged edge words
+    const int scr_cap = (p.wave_lds_emit - 8 * E - 4 * kTileWaves) / 4;
     const int64_t eb = b;
     // global offset: edges of envs [0, b)  (host keeps totals < 2^31)
     int before = 0;
@@ -653,7 +706,7 @@ __global__ __launch_bounds__(kTileBlock) void gsm_emit_tile_kernel(DevParams p) 
     for (int e = tid; e < E; e += kTileBlock) s_pos[e] = p.pos[eb * E + e];
     const int64_t off = tile_sum(before, s_red);
     emit_env(p, EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity}, s_pos, p.row_mask + eb * p.M * p.W, off,
-             s_red);
+             s_red, s_scr, scr_cap, (int32_t)(eb * E));
     if (tid == 0) {
         p.edge_ptr[b] = off;
         if (b == p.B - 1) p.edge_ptr[p.B] = off + p.edge_count[b];

@@ -148,6 +148,15 @@ typedef struct gsm_buffers {
      * GSM_DEGENERATE_NONFINITE if an agent position is not finite (strict
      * mode, or a caller-written state) */
     uint8_t *degenerate;      /* [B] */
+    /* optional, polygon/line assignment warm start (NULL: every per-step
+     * assignment is solved from scratch): the column duals and the matching
+     * of each env's last assignment, kept by the library between launches.
+     * A warm-started assignment is used only when certified to be the unique
+     * optimum — then it IS scipy's result; otherwise the scipy recurrence runs
+     * from scratch. Initialise lsa_col to -1 (lsa_v to 0). */
+    double *lsa_v;            /* [B][N] */
+    int32_t *lsa_col;         /* [B][N] */
+    int32_t *lsa_stats;       /* [B][2] optional counters: certified warm starts, assignments solved */
 } gsm_buffers;
 
 #define GSM_DEGENERATE_COINCIDENT 1

@@ -17,7 +17,7 @@ for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), re
             if "gsm" not in name:
                 continue
             if "step" in name:   # the lagged-emission step kernel: template argument kLag = true
-                short = "lag" if ", true>" in name else "step"
+                short = "lag" if "true>" in name else "step"
             else:
                 short = "emit" if "emit" in name else name[:40]
             acc[short][row["Counter_Name"]].append(float(row["Counter_Value"]))
