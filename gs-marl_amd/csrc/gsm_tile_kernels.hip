@@ -338,7 +338,11 @@ __device__ __forceinline__ int obs_sweep_any(const DevParams &p, const float2 *s
     }
 }
 
-#ifdef GSM_TILE_OCC8   // experiment: force 8 waves/SIMD (spills registers)
+// 8 waves per SIMD: four 512-thread workgroups per CU, so C3's 1024 envs run
+// in one residency round (the compiler's default, 106 SGPRs, allowed 7 waves
+// and three workgroups per CU). Fits without scratch (78 SGPRs, 58 VGPRs);
+// step kernel 23.4 -> 22.0 us at C3.
+#ifndef GSM_TILE_OCC7   // experiment: the compiler's default occupancy
 #define GSM_TILE_ATTR __attribute__((amdgpu_waves_per_eu(8)))
 #else
 #define GSM_TILE_ATTR
