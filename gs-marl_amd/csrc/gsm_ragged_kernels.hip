@@ -528,7 +528,13 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
         float own;
         int nit = 0;
         GSM_STAMP(p, b, 0);
+#ifdef GSM_RAGGED_PRIO   // experiment: the assignment's long dependent chain at raised priority
+        if (s.N >= GSM_RAGGED_PRIO) __builtin_amdgcn_s_setprio(3);
+#endif
         sigma = wave_lsa(s.N, lane, cp, slot, s_cost, &own, lsa_warm, &nit);
+#ifdef GSM_RAGGED_PRIO
+        __builtin_amdgcn_s_setprio(0);
+#endif
         GSM_STAMP(p, b, 1);
 #ifdef GSM_STAMPS
         if (p.stamps && lane == 0) p.stamps[(int64_t)b * 16 + 2] = (uint64_t)nit;
@@ -630,7 +636,12 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
     return edges;
 }
 
-__global__ __launch_bounds__(kBlock) void gsm_step_ragged_kernel(DevParams p) {
+#ifdef GSM_RAGGED_OCC   // experiment: waves per SIMD
+#define GSM_RAGGED_ATTR __attribute__((amdgpu_waves_per_eu(GSM_RAGGED_OCC)))
+#else
+#define GSM_RAGGED_ATTR
+#endif
+__global__ __launch_bounds__(kBlock) GSM_RAGGED_ATTR void gsm_step_ragged_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: env shape, loops and assignment state stay scalar
     // env block of this workgroup (mixed: heaviest first, gsm_abi.hip update_block_order)

@@ -17,12 +17,34 @@ stream provider only); every compute call goes through the C ABI. Layout
 from __future__ import annotations
 
 import ctypes as C
+import os
 from typing import Optional
 
 import torch
 
 from . import _lib
 from .config import EnvConfig
+
+# roctx ranges around every launch call (GSM_ROCTX=1; torch.cuda.nvtx is
+# roctx on ROCm), so rocprofv3 --marker-trace timelines show env.step /
+# reset / observe / graph replays next to their kernels. Off by default.
+_ROCTX = os.environ.get("GSM_ROCTX", "") not in ("", "0")
+
+
+def _ranged(name):
+    def deco(fn):
+        if not _ROCTX:
+            return fn
+
+        def wrapped(*a, **kw):
+            torch.cuda.nvtx.range_push(name)
+            try:
+                return fn(*a, **kw)
+            finally:
+                torch.cuda.nvtx.range_pop()
+        wrapped.__name__, wrapped.__doc__ = fn.__name__, fn.__doc__
+        return wrapped
+    return deco
 
 
 def _require_gpu(device) -> torch.device:
@@ -127,6 +149,7 @@ class GpuBatchEnv:
         return out
 
     # ------------------------------------------------------------------- API
+    @_ranged("gsm.reset")
     def reset(self, seed: Optional[int] = None, env_mask: Optional[torch.Tensor] = None,
               sync_edges: bool = True) -> dict:
         """Re-lay-out the masked envs (all if None). With ``seed`` the episode
@@ -182,6 +205,7 @@ class GpuBatchEnv:
             o.edge_index, o.edge_attr, o.edge_capacity = ei.data_ptr(), ea.data_ptr(), int(ei.shape[1])
         return o
 
+    @_ranged("gsm.step")
     def step(self, actions: torch.Tensor, sync_edges: bool = True, out: Optional[dict] = None) -> dict:
         """One env.step. With ``out`` (a dict of device tensors, e.g. a rollout
         buffer slot) the step writes those outputs there instead (no copies)."""
@@ -196,6 +220,7 @@ class GpuBatchEnv:
         self._chk(self.lib.gsm_step_into(self._h, a, fmt, C.byref(o), self._stream()), "gsm_step_into")
         return out
 
+    @_ranged("gsm.observe")
     def observe(self, sync_edges: bool = True, out: Optional[dict] = None) -> dict:
         if out is None:
             self._chk(self.lib.gsm_observe(self._h, self._stream()), "gsm_observe")
@@ -267,6 +292,7 @@ class GpuBatchEnv:
         self._chk(self.lib.gsm_graph_capture_into(self._h, int(slot), C.c_void_p(a.data_ptr()), stride,
                                                   a.shape[0], len(outs), fmt, arr), "gsm_graph_capture_into")
 
+    @_ranged("gsm.replay")
     def replay(self, slot: int = 0) -> None:
         self._chk(self.lib.gsm_graph_launch(self._h, int(slot), self._stream()), "gsm_graph_launch")
 
