@@ -243,8 +243,8 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
     p->env_base = c->env_base;
     p->strict = c->strict_degenerate != 0;
     if (p->path == gsm::kPathRagged) {
-        // assignment cost matrix [N][N] fp32 + staged entity positions [E]
-        p->wave_lds_step = align16(4 * N * N + 8 * p->E);
+        // assignment scratch (cost matrix, duals) + staged entity positions [E]
+        p->wave_lds_step = align16(gsm::lsa_lds_bytes(N) + 8 * p->E);
         p->wave_lds_emit = align16(8 * p->E);
     } else if (p->path == gsm::kPathSeg) {
         // positions + staged node-feature rows of the wave's G envs

@@ -21,6 +21,25 @@ __device__ __forceinline__ uint32_t shl1_add_lane(uint32_t own, uint64_t lanes) 
     return r;
 }
 
+// v_cndmask with a wave-uniform lane mask held in SGPRs (a ballot, a bit
+// set): lanes whose bit of m is set take a, the others b. The mask is used as
+// is, without the per-lane bit extraction (v_and + v_cmp) the compiler emits
+// for a select on ((m >> lane) & 1).
+__device__ __forceinline__ uint32_t sel_lanes(uint64_t m, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(r) : "v"(b), "v"(a), "s"(m));
+    return r;
+}
+__device__ __forceinline__ int sel_lanes(uint64_t m, int a, int b) {
+    return (int)sel_lanes(m, (uint32_t)a, (uint32_t)b);
+}
+__device__ __forceinline__ double sel_lanes(uint64_t m, double a, double b) {
+    const uint64_t ua = (uint64_t)__double_as_longlong(a), ub = (uint64_t)__double_as_longlong(b);
+    const uint32_t lo = sel_lanes(m, (uint32_t)ua, (uint32_t)ub);
+    const uint32_t hi = sel_lanes(m, (uint32_t)(ua >> 32), (uint32_t)(ub >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 // Orders LDS traffic between the lanes of one wave: LDS ops of a wave execute
 // in order, so only compiler motion has to be fenced.
 __device__ __forceinline__ void wave_sync() {
@@ -115,7 +134,12 @@ __device__ __forceinline__ int collider_entity(int c, int N) { return c < N ? c 
 
 __device__ __forceinline__ float2 layout_pos(const DevParams &p, uint32_t gid, uint32_t ep,
                                              uint32_t e) {
-    const Philox4 x = philox4x32_10(e, ep, gid, kTagLayout, p.seed_lo, p.seed_hi);
+    // keys in VGPRs: the (cold) reset path otherwise holds Philox's whole
+    // wave-uniform key schedule in SGPRs, which set the step kernels' SGPR
+    // count and hence their occupancy
+    uint32_t k0 = p.seed_lo, k1 = p.seed_hi;
+    asm volatile("" : "+v"(k0), "+v"(k1));
+    const Philox4 x = philox4x32_10(e, ep, gid, kTagLayout, k0, k1);
     return make_float2(u01(x.x0) * p.twoL - p.L, u01(x.x1) * p.twoL - p.L);
 }
 

@@ -186,9 +186,36 @@ struct LsaWarm {
 //    start cannot use):
 //  * cold: scipy's rectangular_lsap recurrence from scratch (oracle/lsa_ref.py),
 //    rows in order, with its tie rules.
-__device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, float *own, LsaWarm w,
-                        int *iters = nullptr) {
+#ifdef GSM_STAMPS   // diagnostic builds: s_memtime at the assignment's phase boundaries
+#define LSA_T(k)                                                                   \
+    do {                                                                           \
+        unsigned long long t_;                                                     \
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory"); \
+        if (tm && lane == 0) tm[k] = t_;                                           \
+    } while (0)
+#else
+#define LSA_T(k) do { } while (0)
+#endif
+// LDS of the assignment (lsa_lds_bytes): C row-major at an odd stride S
+// (row i, column j at i*S + j: a lane per row reads column j of 32 rows from
+// 32 distinct banks), the column duals, and a column -> row scratch.
+struct LsaLds {
+    float *cost;   // [roundup8(N_max)][S]
+    double *v;     // [32]
+    int *keep;     // [32]
+    int S;
+};
+__device__ __forceinline__ LsaLds lsa_lds(unsigned char *lds, int nmax) {
+    const int S = lsa_stride(nmax);
+    const int cb = (lsa_cost_bytes(nmax) + 15) & ~15;
+    return LsaLds{(float *)lds, (double *)(lds + cb), (int *)(lds + cb + 8 * kRaggedMaxAgents), S};
+}
+
+__device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &sl, float *own, LsaWarm w,
+                        int *iters = nullptr, uint64_t *tm = nullptr) {
     const bool col = lane < N;
+    float *const s_cost = sl.cost;
+    const int S = sl.S;
     // a non-finite agent position (strict mode, App. A S16; or a caller-written
     // state) has no assignment (scipy raises on such a cost matrix): slot -1,
     // cost NaN
@@ -202,20 +229,30 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
 #endif
     // column `lane` of C held in registers, C[i][lane] picked by the
     // wave-uniform row i (s_set_gpr_idx): no LDS round trip in the path loop;
-    // the LDS copy serves the final cost lookup
+    // the LDS copy serves the row-parallel passes and the final cost lookup.
+    // Rows in groups of 8 with no per-row branch, so the (correctly rounded)
+    // square roots of a group are independent instructions; rows >= N of the
+    // last group are computed and never read.
     float ccol[kRaggedMaxAgents];
 #pragma unroll
-    for (int i = 0; i < kRaggedMaxAgents; ++i) {
-        float c = 0.0f;
-        if (i < N) {
-            const float2 pi = rl_f2(pa, i);
-            const float dx = pi.x - slot.x, dy = pi.y - slot.y;
-            c = sqrtf(dx * dx + dy * dy);
-            if (col) s_cost[i * N + lane] = c;
+    for (int i0 = 0; i0 < kRaggedMaxAgents; i0 += 8) {
+        if (i0 < N) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const float2 pi = rl_f2(pa, i0 + k);
+                const float dx = pi.x - slot.x, dy = pi.y - slot.y;
+                ccol[i0 + k] = sqrtf(dx * dx + dy * dy);
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                if (col) s_cost[(i0 + k) * S + lane] = ccol[i0 + k];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) ccol[i0 + k] = 0.0f;
         }
-        ccol[i] = c;
     }
     wave_sync();
+    LSA_T(0);
     const double kInf = __builtin_inf();
     double u = 0.0, v = 0.0;
     int col4row = -1, row4col = -1;
@@ -237,6 +274,10 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
         // minimum, else an exact f64 reduction among the near ones) -> the
         // column's row.
         uint64_t remm = colmask, srm = 0;
+#ifdef GSM_STAMPS
+        unsigned long long ta_, tb_, tc_;
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(ta_)::"memory");
+#endif
         // a square problem reaches a free column within N scans; the bound
         // only guarantees termination should the invariants ever break
         for (int guard = 0; guard < N; ++guard) {
@@ -245,11 +286,12 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
 #endif
             srm |= 1ull << i;
             const double ui = rl_d(u, i);
-            const bool rem = (remm >> lane) & 1;
             const double r = minVal + (double)ccol[i] - ui - v;
-            const bool upd = rem && r < spc;
-            path = upd ? i : path;
-            spc = upd ? r : spc;
+            // selects on SGPR lane masks (remm, the update ballot), no per-lane
+            // bit extraction on the chain
+            const uint64_t upd = __builtin_amdgcn_ballot_w64(r < spc) & remm;
+            path = sel_lanes(upd, i, path);
+            spc = sel_lanes(upd, r, spc);
             // scipy scans `remaining` in order and keeps the first minimum
             // unless a later equal one is unassigned: the last unassigned
             // minimum in scan order if any, else the first minimum. The
@@ -260,7 +302,8 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
             // several (near or exact ties) take the f64 reduction among them;
             // exact ties then take one more reduction over key = 64 + pos
             // (unassigned) or 63 - pos (assigned), larger key winning.
-            const int key = rem ? f32_order_key((float)spc + 0.0f) : 0x7fffffff;
+            // Lanes outside `remaining` carry INT_MAX, above every finite key.
+            const int key = sel_lanes(remm, f32_order_key((float)spc + 0.0f), 0x7fffffff);
             const int kmin = min32_i(key);
             const uint64_t near = __builtin_amdgcn_ballot_w64(key == kmin) & remm;
             if (!near) break;
@@ -270,11 +313,11 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
                 jsel = first_lane(near);
                 m = rl_d(spc, jsel);
             } else {
-                m = min32((near >> lane) & 1 ? spc : kInf);
+                m = min32(sel_lanes(near, spc, kInf));
                 const uint64_t cand = __builtin_amdgcn_ballot_w64(spc == m) & remm;
                 jsel = first_lane(cand);
                 if (cand & (cand - 1)) {
-                    const int tkey = (cand >> lane) & 1 ? (row4col == -1 ? 64 + rpos : 63 - rpos) : -1;
+                    const int tkey = sel_lanes(cand, row4col == -1 ? 64 + rpos : 63 - rpos, -1);
                     const int kb = max32(tkey);
                     jsel = first_lane(__builtin_amdgcn_ballot_w64(tkey == kb));
                 }
@@ -284,13 +327,18 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
             const int at = __builtin_amdgcn_readlane(rpos, jsel);
             remm &= ~(1ull << jsel);
             nrem -= 1;
-            rpos = (rem && lane != jsel && rpos == nrem) ? at : rpos;   // remaining[index] = remaining[--n]
+            // remaining[index] = remaining[--n]: the lane at the last position
+            // moves to jsel's
+            rpos = sel_lanes(__builtin_amdgcn_ballot_w64(rpos == nrem) & remm, at, rpos);
             if (r4c < 0) {
                 sink = jsel;
                 break;
             }
             i = r4c;
         }
+#ifdef GSM_STAMPS
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tb_)::"memory");
+#endif
         if (sink < 0) return false;   // unreachable for finite costs
         const bool SR = (srm >> lane) & 1, SC = ((colmask & ~remm) >> lane) & 1;
         // dual update (before augmenting: col4row is the previous matching)
@@ -308,6 +356,13 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
             j = nj;
             if (pi_ == cur) break;
         }
+#ifdef GSM_STAMPS   // path-loop and update cycles, summed over the augments
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tc_)::"memory");
+        if (tm && lane == 0) {
+            tm[6] += tb_ - ta_;
+            tm[7] += tc_ - tb_;
+        }
+#endif
         return true;
     };
 
@@ -316,33 +371,45 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
     // alternating cycle of tight pairs (r <= 1e-9) — the graph with an arc
     // from row i to the row holding column j for every tight unmatched (i, j)
     // is acyclic (peeled sink by sink)
-    auto certified = [&]() -> bool {
+    auto certified = [&](double tau = 1e-9) -> bool {
+        // row-parallel: lane i checks row i against the column duals in LDS
+        if (lane < kRaggedMaxAgents) sl.v[lane] = v;
+        wave_sync();
         bool good = true;
         uint32_t tight = 0;   // lane i: tight unmatched columns of row i
-        for (int i = 0; i < N; ++i) {
-            const double ui = rl_d(u, i);
-            const int ci = __builtin_amdgcn_readlane(col4row, i);
-            const double r = (double)ccol[i] - ui - v;
-            good &= !col || (lane == ci ? fabs(r) <= 1e-11 : r >= -1e-11);
-            const uint64_t t = __builtin_amdgcn_ballot_w64(col && lane != ci && r <= 1e-9);
-            tight = writelane_u32((uint32_t)t, (uint32_t)i, tight);
+        if (col) {
+            const float *crow = s_cost + lane * S;
+            const int ci = col4row;
+            for (int j = 0; j < N; ++j) {
+                const double r = (double)crow[j] - u - sl.v[j];
+                good &= j == ci ? fabs(r) <= 1e-11 : r >= -1e-11;
+                tight |= (j != ci && r <= tau) ? 1u << j : 0u;
+            }
         }
-        if (!__all(good)) return false;
+        if (!__all(good)) {
+#ifdef GSM_STAMPS   // diagnostic builds: why the certificate failed (bits 24+)
+            if (iters) *iters |= 2 << 24;
+#endif
+            return false;
+        }
         uint64_t rows = colmask, cols = colmask;   // rows not yet peeled, their columns
         for (int it = 0; it < N && rows; ++it) {
             const bool sink = ((rows >> lane) & 1) && !(tight & (uint32_t)cols);
-            const uint64_t S = __builtin_amdgcn_ballot_w64(sink);
-            if (!S) break;                       // every remaining row is on a cycle
-            rows &= ~S;
-            cols &= ~__builtin_amdgcn_ballot_w64(col && row4col >= 0 && ((S >> row4col) & 1));
+            const uint64_t sinks = __builtin_amdgcn_ballot_w64(sink);
+            if (!sinks) break;                   // every remaining row is on a cycle
+            rows &= ~sinks;
+            cols &= ~__builtin_amdgcn_ballot_w64(col && row4col >= 0 && ((sinks >> row4col) & 1));
         }
+#ifdef GSM_STAMPS
+        if (iters && tau == 1e-9) *iters |= (rows == 0 ? 1 : 3) << 24;
+#endif
         return rows == 0;
     };
 
     bool solved = false;
     if (w.v) {
-        const double v0 = col ? w.v[lane] : 0.0;
-        const int c0 = col ? w.col[lane] : -1;
+        const double v0 = col ? w.v[lane] : 0.0;    // column duals: lane = column
+        const int c0 = col ? w.col[lane] : -1;      // previous matching: lane = row
         if (__all(!col || __builtin_isfinite(v0))) {
             // feasible row duals from the previous v; rows whose previous
             // column still attains their minimum keep it, the others are
@@ -350,32 +417,56 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
             // previous matching and restoring feasibility by Bellman-Ford on
             // v certified only 5% of N = 24 polygon steps under random
             // actions — the optimum moves — and cost more than it saved.)
+            // Row-parallel: lane i scans row i of C in LDS (independent
+            // iterations; u_i = min_j (C[i][j] - v_j) is exact in any order).
             v = v0;
-            uint64_t taken = 0, freerows = 0;
-            for (int i = 0; i < N; ++i) {
-                const double r = col ? (double)ccol[i] - v : kInf;
-                const int key = col ? f32_order_key((float)r + 0.0f) : 0x7fffffff;
-                const int kmin = min32_i(key);
-                const uint64_t near = __builtin_amdgcn_ballot_w64(key == kmin) & colmask;
-                const double m = !(near & (near - 1)) ? rl_d(r, first_lane(near))
-                                                      : min32((near >> lane) & 1 ? r : kInf);
-                if (lane == i) u = m;
-                const int ci = __builtin_amdgcn_readlane(c0, i);
-                const bool keep = ci >= 0 && ci < N && !((taken >> ci) & 1) && rl_d(r, ci) == m;
-                if (keep) {
-                    taken |= 1ull << ci;
-                    if (lane == i) col4row = ci;
-                    if (lane == ci) row4col = i;
-                } else {
-                    freerows |= 1ull << i;
+            if (lane < kRaggedMaxAgents) {
+                sl.v[lane] = v0;
+                sl.keep[lane] = -1;
+            }
+            wave_sync();
+            double m0 = kInf, m1 = kInf, rc = kInf;
+            if (col) {
+                const float *crow = s_cost + lane * S;
+                int j = 0;
+                for (; j + 1 < N; j += 2) {
+                    const double r0 = (double)crow[j] - sl.v[j];
+                    const double r1 = (double)crow[j + 1] - sl.v[j + 1];
+                    m0 = fmin(m0, r0);
+                    m1 = fmin(m1, r1);
+                    rc = j == c0 ? r0 : (j + 1 == c0 ? r1 : rc);
+                }
+                if (j < N) {
+                    const double r0 = (double)crow[j] - sl.v[j];
+                    m0 = fmin(m0, r0);
+                    rc = j == c0 ? r0 : rc;
                 }
             }
+            const double m = fmin(m0, m1);
+            u = col ? m : 0.0;
+            // a row keeps its previous column when that column attains its
+            // minimum (c0 is a matching, so no column is claimed twice; a
+            // duplicate would keep one claimant, any one: the result is used
+            // only if certified unique)
+            const bool want = col && c0 >= 0 && c0 < N && rc == m;
+            if (want) sl.keep[c0] = lane;
+            wave_sync();
+            const bool kept = want && sl.keep[c0] == lane;
+            col4row = kept ? c0 : -1;
+            row4col = col ? sl.keep[lane] : -1;
+            const uint64_t freerows = __builtin_amdgcn_ballot_w64(col && !kept);
 #ifdef GSM_STAMPS   // diagnostic builds: rows the warm start re-augments (high half)
             if (iters) *iters += __popcll(freerows) << 16;
 #endif
+            LSA_T(1);
             bool ok = true;
             for (uint64_t fr = freerows; fr && ok; fr &= fr - 1) ok = augment(first_lane(fr));
+            LSA_T(2);
             solved = ok && certified();
+            LSA_T(3);
+#ifdef GSM_STAMPS   // diagnostic: would a 1e-13 tight threshold certify it? (code 4)
+            if (ok && !solved && iters && ((*iters >> 24) & 0xff) == 3 && certified(1e-13)) *iters += 1 << 24;
+#endif
         }
         if (w.stats && lane == 0) {
             w.stats[0] += solved ? 1 : 0;
@@ -394,7 +485,7 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
         w.v[lane] = v;
         w.col[lane] = col4row;
     }
-    *own = col && col4row >= 0 ? s_cost[lane * N + col4row] : 0.0f;
+    *own = col && col4row >= 0 ? s_cost[lane * S + col4row] : 0.0f;
     return col ? col4row : -1;
 }
 
@@ -404,8 +495,8 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, float *s_cost, 
 __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, unsigned char *lds) {
     const int Nmax = p.N, Tmax = p.T, Emax = p.E, Mmax = p.M;
     const int64_t eb = b;
-    float *s_cost = (float *)lds;                               // [N_max][N_max]
-    float2 *s_pos = (float2 *)(lds + 4 * Nmax * Nmax);          // [E] staged rows
+    const LsaLds s_lsa = lsa_lds(lds, Nmax);                    // assignment scratch
+    float2 *s_pos = (float2 *)(lds + lsa_lds_bytes(Nmax));      // [E] staged rows
     float2 *pos_b = p.pos + eb * Emax;
     const bool do_reset = p.mode == kModeReset && (p.env_mask == nullptr || p.env_mask[b] != 0);
     const LsaWarm lsa_warm{p.lsa_v ? p.lsa_v + eb * Nmax : nullptr, p.lsa_col ? p.lsa_col + eb * Nmax : nullptr,
@@ -531,7 +622,11 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
 #ifdef GSM_RAGGED_PRIO   // experiment: the assignment's long dependent chain at raised priority
         if (s.N >= GSM_RAGGED_PRIO) __builtin_amdgcn_s_setprio(3);
 #endif
-        sigma = wave_lsa(s.N, lane, cp, slot, s_cost, &own, lsa_warm, &nit);
+#ifdef GSM_STAMPS
+        sigma = wave_lsa(s.N, lane, cp, slot, s_lsa, &own, lsa_warm, &nit, p.stamps ? p.stamps + (int64_t)b * 16 + 4 : nullptr);
+#else
+        sigma = wave_lsa(s.N, lane, cp, slot, s_lsa, &own, lsa_warm, &nit);
+#endif
 #ifdef GSM_RAGGED_PRIO
         __builtin_amdgcn_s_setprio(0);
 #endif
@@ -563,7 +658,7 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
             if (s.scn != kScnNav) {
                 slot = slot_of(p, s, lane, tp);
                 float own;
-                sigma = wave_lsa(s.N, lane, cp, slot, s_cost, &own, lsa_warm);
+                sigma = wave_lsa(s.N, lane, cp, slot, s_lsa, &own, lsa_warm);
             }
         }
     }
@@ -633,6 +728,9 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
         p.edge_count[b] = edges;
         if (relaid) p.env_shape[b] = s.N | (s.scn << 8);
     }
+#ifdef GSM_STAMPS
+    if (p.stamps && lane == 0) p.stamps[(int64_t)b * 16 + 3] = (uint64_t)(s.N | (s.scn << 8));
+#endif
     return edges;
 }
 
@@ -648,7 +746,9 @@ __global__ __launch_bounds__(kBlock) GSM_RAGGED_ATTR void gsm_step_ragged_kernel
     const int blk = p.block_order ? p.block_order[blockIdx.x] : (int)blockIdx.x;
     const int b = blk * kWavesPerBlock + wave;
     int edges = 0;
+    GSM_RSTAMP(p, b, 8);
     if (b < p.B) edges = ragged_env_step(p, b, lane, smem + wave * p.wave_lds_step);
+    GSM_RSTAMP(p, b, 9);
     int *s_bc = (int *)(smem + kWavesPerBlock * p.wave_lds_step);
     if (lane == 0) s_bc[wave] = edges;
     __syncthreads();

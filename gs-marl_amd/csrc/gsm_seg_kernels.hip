@@ -599,11 +599,15 @@ __device__ __forceinline__ void block_emit(const DevParams &p, const Shape<kN, k
                                            int scr_cap) {
     const int first = blockIdx.x * kWavesPerBlock * s.G;
     const int acc = wave_total(pre.acc);
-    if (L.lane == 0) s_red[L.wave] = acc;
     const int incl_k = wave_scan(pre.cnt_k);     // envs of this block in order
+#ifdef GSM_ABL_NO_LAGBAR   // timing-only: no workgroup exchange of the prefix
+    int64_t base = acc;
+#else
+    if (L.lane == 0) s_red[L.wave] = acc;
     __syncthreads();
     int64_t base = 0;
     for (int q = 0; q < kWavesPerBlock; ++q) base += s_red[q];
+#endif
     int my_cnt, before;
     if constexpr (kG == 1) {
         my_cnt = __builtin_amdgcn_readlane(pre.cnt_k, L.wave);

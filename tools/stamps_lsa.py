@@ -30,8 +30,13 @@ s = st.cpu().numpy().astype(np.int64)[:B]
 cyc, raw = s[:, 1] - s[:, 0], s[:, 2]
 it, free = raw & 0xFFFF, (raw >> 16) & 0xFF
 ok = cyc > 0
+ph = np.diff(s[:, 4:8], axis=1)   # row loop, augments, certificate (s_memtime cycles)
+pre = s[:, 4] - s[:, 0]           # cost matrix
 print(json.dumps(dict(scenario=scn, N=N, B=B, envs=int(ok.sum()), lsa_cycles_median=float(np.median(cyc[ok])),
                       lsa_cycles_max=int(cyc[ok].max()),
                       iters_median=float(np.median(it[ok])), iters_max=int(it[ok].max()),
                       free_rows_median=float(np.median(free[ok])), free_rows_max=int(free[ok].max()),
-                      warm_stats=env.lsa_warm_stats())))
+                      warm_stats=env.lsa_warm_stats(),
+                      phase_cycles_median=dict(cost=float(np.median(pre[ok])), rows=float(np.median(ph[ok, 0])),
+                                               augment=float(np.median(ph[ok, 1])), certify=float(np.median(ph[ok, 2])),
+                                               aug_loops=float(np.median(s[ok, 10])), aug_updates=float(np.median(s[ok, 11]))))))
