@@ -21,6 +21,18 @@ __device__ __forceinline__ uint32_t shl1_add_lane(uint32_t own, uint64_t lanes) 
     return r;
 }
 
+// The launch's DevParams read back from the kernarg segment at the point of
+// use: fields loaded through this view are fresh scalar loads there (the asm
+// hides that the pointer is the one read at kernel entry), so base pointers
+// used only by a kernel's final stores do not hold SGPRs across the kernel.
+// Valid in kernels whose first argument is the DevParams (all of them).
+typedef const __attribute__((address_space(4))) DevParams KernargParams;
+__device__ __forceinline__ KernargParams &late_params() {
+    KernargParams *kp = (KernargParams *)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(kp));
+    return *kp;
+}
+
 // v_cndmask with a wave-uniform lane mask held in SGPRs (a ballot, a bit
 // set): lanes whose bit of m is set take a, the others b. The mask is used as
 // is, without the per-lane bit extraction (v_and + v_cmp) the compiler emits
@@ -193,7 +205,8 @@ __device__ __forceinline__ bool strict_bad(int self, float2 a, int N, int M, Pos
 // parity bar). The raw base-2 v_exp_f32 / v_log_f32 are used
 // directly: 1 + e lies in (1, 2], so the library log's denormal scaling
 // (a dozen VALU per pair) is never needed, and an exp2 underflow is e = 0.
-__device__ __forceinline__ float contact_scale(const DevParams &p, float d2, float dmin) {
+template <typename Params>   // DevParams or its kernarg view (late_params)
+__device__ __forceinline__ float contact_scale(const Params &p, float d2, float dmin) {
     constexpr float kLog2e = 1.44269504088896341f, kLn2 = 0.693147180559945309f;
     const float d = __builtin_amdgcn_sqrtf(d2);
     const float D = dmin - d;

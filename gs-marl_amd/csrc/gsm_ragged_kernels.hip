@@ -263,6 +263,10 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
     // false if no free column was reached (never for finite costs).
     auto augment = [&](int cur) -> bool {
         double spc = kInf;
+        // 32-bit order key of spc (below), kept beside it: the key of a new r
+        // is formed alongside the comparison instead of after the select;
+        // INT_MAX once the column leaves `remaining`
+        int key = sel_lanes(colmask, f32_order_key(__builtin_inff()), 0x7fffffff);
         int path = -1;
         int rpos = N - 1 - lane;     // position in scipy's `remaining` list (filled in reverse)
         int nrem = N;
@@ -289,9 +293,11 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
             const double r = minVal + (double)ccol[i] - ui - v;
             // selects on SGPR lane masks (remm, the update ballot), no per-lane
             // bit extraction on the chain
+            const int rkey = f32_order_key((float)r + 0.0f);
             const uint64_t upd = __builtin_amdgcn_ballot_w64(r < spc) & remm;
             path = sel_lanes(upd, i, path);
             spc = sel_lanes(upd, r, spc);
+            key = sel_lanes(upd, rkey, key);
             // scipy scans `remaining` in order and keeps the first minimum
             // unless a later equal one is unassigned: the last unassigned
             // minimum in scan order if any, else the first minimum. The
@@ -303,7 +309,6 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
             // exact ties then take one more reduction over key = 64 + pos
             // (unassigned) or 63 - pos (assigned), larger key winning.
             // Lanes outside `remaining` carry INT_MAX, above every finite key.
-            const int key = sel_lanes(remm, f32_order_key((float)spc + 0.0f), 0x7fffffff);
             const int kmin = min32_i(key);
             const uint64_t near = __builtin_amdgcn_ballot_w64(key == kmin) & remm;
             if (!near) break;
@@ -326,6 +331,7 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
             const int r4c = __builtin_amdgcn_readlane(row4col, jsel);
             const int at = __builtin_amdgcn_readlane(rpos, jsel);
             remm &= ~(1ull << jsel);
+            key = sel_lanes(1ull << jsel, 0x7fffffff, key);
             nrem -= 1;
             // remaining[index] = remaining[--n]: the lane at the last position
             // moves to jsel's

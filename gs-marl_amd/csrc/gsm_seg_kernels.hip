@@ -743,8 +743,6 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     // per-env base pointers: wave-uniform (scalar) when G = 1; lane offsets
     // below are 32-bit
     const int64_t eb = kG == 1 ? (wave_live ? L.b : 0) : (L.live ? L.b : 0);
-    float2 *const pos_b = p.pos + eb * E;
-    float2 *const vel_b = p.vel + eb * N;
     const uint32_t um = (uint32_t)m;
 
     SegIn inf = in;
@@ -780,8 +778,9 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     if constexpr (kLag) {
         // the previous step's edges: its positions (staged above) and row masks
         // scratch: the staged node-feature / column-pair area (free until the sweep)
-        block_emit<kN, kNo, kG>(p, s, L, s_pos, oo, lag_pre, s_lag, p.lag.edge_ptr,
-                                EdgeSink{p.lag.edge_index, p.lag.edge_attr, p.lag.cap}, (uint32_t *)s_nf,
+        KernargParams &q = late_params();
+        block_emit<kN, kNo, kG>(p, s, L, s_pos, oo, lag_pre, s_lag, q.lag.edge_ptr,
+                                EdgeSink{q.lag.edge_index, q.lag.edge_attr, q.lag.cap}, (uint32_t *)s_nf,
                                 (p.wave_lds_step - 8 * G * E) / 4);
     }
     GSM_STAMP(p, wid, 2);
@@ -804,6 +803,8 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     if (p.mode == kModeStep) {
         // apply_environment_force over the candidates found on these positions
         // by the previous observation pass, then integrate_state (App. A S6)
+        // physics constants read here (kernarg view), not held from the entry
+        KernargParams &pc = late_params();
         if (L.agent) {
             const float2 pi = s_pos[m];
             float Fx = u.x, Fy = u.y;
@@ -818,33 +819,34 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
                 const float2 pj = s_pos[row_entity(c, N)];
                 const float dx = pi.x - pj.x, dy = pi.y - pj.y;
                 const float d2 = dx * dx + dy * dy;
-                const float f = contact_scale(p, d2, ag ? p.dmin_aa : p.dmin_ao);
+                const float f = contact_scale(pc, d2, ag ? pc.dmin_aa : pc.dmin_ao);
                 Fx += f * dx;
                 Fy += f * dy;
             }
-            if (p.strict && strict_bad(m, pi, N, M, [&](int c) { return s_pos[row_entity(c, N)]; })) {
+            if (pc.strict && strict_bad(m, pi, N, M, [&](int c) { return s_pos[row_entity(c, N)]; })) {
                 Fx = __builtin_nanf("");   // App. A S16 strict: MPE's 0/0 force
                 Fy = __builtin_nanf("");
             }
-            v.x = v.x * p.omd;
-            v.y = v.y * p.omd;
-            v.x = v.x + (Fx * p.inv_mass) * p.dt;
-            v.y = v.y + (Fy * p.inv_mass) * p.dt;
-            if (p.max_speed > 0.0f) {
+            const float dt = pc.dt, max_speed = pc.max_speed;
+            v.x = v.x * pc.omd;
+            v.y = v.y * pc.omd;
+            v.x = v.x + (Fx * pc.inv_mass) * dt;
+            v.y = v.y + (Fy * pc.inv_mass) * dt;
+            if (max_speed > 0.0f) {
                 const float sp = sqrtf(v.x * v.x + v.y * v.y);
-                if (sp > p.max_speed) {
-                    v.x = v.x / sp * p.max_speed;
-                    v.y = v.y / sp * p.max_speed;
+                if (sp > max_speed) {
+                    v.x = v.x / sp * max_speed;
+                    v.y = v.y / sp * max_speed;
                 }
             }
             float2 np;
-            np.x = pi.x + v.x * p.dt;
-            np.y = pi.y + v.y * p.dt;
+            np.x = pi.x + v.x * dt;
+            np.y = pi.y + v.y * dt;
             s_pos[m] = np;
         }
         wave_sync();
         t += 1;
-        done = L.live && t >= p.EL;
+        done = L.live && t >= pc.EL;
     }
     GSM_STAMP(p, wid, 3);
 
@@ -873,8 +875,9 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     const int ci = L.agent ? ccnt : 0;
     const int csum = seg_total<kG>(ci, L, M);
     if (L.agent) {
-        (p.reward + eb * N)[um] = p.shared_reward ? rsum : r;
-        (p.cost + eb * N)[um] = (float)ci;
+        KernargParams &q = late_params();
+        (q.reward + eb * N)[um] = p.shared_reward ? rsum : r;
+        (q.cost + eb * N)[um] = (float)ci;
     }
     if (p.shared_reward) rsum *= (float)N;
     bool relaid = reset;                                    // layout changed in this launch
@@ -910,12 +913,16 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     // ---- outputs and state. Node features: agent rows every step; goal and
     // obstacle rows (static within an episode) only when the layout is new or
     // on an observe. Rows are staged in LDS and stored lane-linear.
+    // base pointers of the final stores: read here, not held from the entry
+    KernargParams &q = late_params();
+    float2 *const pos_b = q.pos + eb * E;
+    float2 *const vel_b = q.vel + eb * N;
     const bool any_statics = p.mode != kModeStep || p.nf_full || __any(relaid);
     // one env per wave: rows go straight to HBM (each lane its 28-byte row,
     // the wave's rows contiguous); G > 1: staged in LDS, stored lane-linear
     constexpr bool kDirectNf = kG == 1;
     if (L.live) {
-        float *nf = kDirectNf ? p.node_feat + eb * E * 7 : s_nf + segc * E * 7;
+        float *nf = kDirectNf ? q.node_feat + eb * E * 7 : s_nf + segc * E * 7;
         if (L.agent) {
             const float2 g = s_pos[N + m];
             store_row(nf + m * 7, v, pm, make_float2(g.x - pm.x, g.y - pm.y), 0.0f);
@@ -930,8 +937,8 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
             pos_b[um] = pm;
         }
         if (L.agent && (p.mode == kModeStep || relaid)) vel_b[um] = v;
-        if (L.agent) (p.contact_mask + eb * N)[um] = cand;
-        (p.row_mask + eb * M)[um] = row;
+        if (L.agent) (q.contact_mask + eb * N)[um] = cand;
+        (q.row_mask + eb * M)[um] = row;
     }
     if constexpr (!kDirectNf) {
         wave_sync();
@@ -941,7 +948,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
             // per env, not per lane: idle lanes of the env's wave copy too
             const bool full_rows = p.mode != kModeStep || p.nf_full || (kG == 1 ? __any(relaid) : __shfl(relaid, g * M));
             const int len = (full_rows ? E : N) * 7;
-            float *dst = p.node_feat + (int64_t)(b0 + g) * E * 7;
+            float *dst = q.node_feat + (int64_t)(b0 + g) * E * 7;
             const float *src = s_nf + g * E * 7;
 #ifdef GSM_ABL_NO_NF   // timing-only
             if (len > 0) continue;
@@ -958,7 +965,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     // App. A S16 flags of the final state: a coincident pair (from the sweep),
     // an agent at a non-finite position
     uint8_t deg = 0;
-    if (p.degenerate) {
+    if (q.degenerate) {
         const uint64_t nb = __ballot(L.agent && nonfinite2(pm));
         const uint64_t segm = M >= 64 ? ~0ull : ((1ull << M) - 1);
         deg = (uint8_t)((coinc ? kDegCoincident : 0) | (((nb >> L.base) & segm) ? kDegNonfinite : 0));
@@ -969,23 +976,23 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     if constexpr (kG == 1) {
         wave_edges = wave_total(edges);
         if (wave_live && L.lane == 0) {
-            p.step_count[L.b] = t;
-            p.episode[L.b] = ep;
-            p.ep_acc[L.b] = acc;
-            p.done[L.b] = done ? 1 : 0;
-            p.edge_count[L.b] = wave_edges;
-            if (p.degenerate) p.degenerate[L.b] = deg;
+            q.step_count[L.b] = t;
+            q.episode[L.b] = ep;
+            q.ep_acc[L.b] = acc;
+            q.done[L.b] = done ? 1 : 0;
+            q.edge_count[L.b] = wave_edges;
+            if (q.degenerate) q.degenerate[L.b] = deg;
         }
     } else {
         wave_edges = wave_sum(edges);
         const int env_edges = seg_total<kG>(edges, L, M);
         if (L.live && m == 0) {
-            p.step_count[L.b] = t;
-            p.episode[L.b] = ep;
-            p.ep_acc[L.b] = acc;
-            p.done[L.b] = done ? 1 : 0;
-            p.edge_count[L.b] = env_edges;
-            if (p.degenerate) p.degenerate[L.b] = deg;
+            q.step_count[L.b] = t;
+            q.episode[L.b] = ep;
+            q.ep_acc[L.b] = acc;
+            q.done[L.b] = done ? 1 : 0;
+            q.edge_count[L.b] = env_edges;
+            if (q.degenerate) q.degenerate[L.b] = deg;
         }
     }
     GSM_STAMP(p, wid, 7);
@@ -1016,7 +1023,7 @@ __global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevP
         if (threadIdx.x == 0) {
             int q = 0;
             for (int k = 0; k < kWavesPerBlock; ++k) q += s_bc[k];
-            p.block_edge_sum[blockIdx.x] = q;
+            late_params().block_edge_sum[blockIdx.x] = q;
         }
     }
     GSM_RSTAMP(p, wid, 9);

@@ -39,5 +39,8 @@ for name, rows, phases in (("step", s[: nb * 4], 8), ("emit", s[nb * 4:], 5)):
         start_spread_us=float((rt0.max() - rt0.min()) / 100.0),
         span_us=float((rt1.max() - rt0.min()) / 100.0),
         wave_lifetime_us_median=float(np.median(rt1 - rt0) / 100.0),
+        phase_cycles_p90=[int(x) for x in np.percentile(d, 90, axis=0)],
+        start_us_pct=[float(x) for x in np.percentile((rt0 - rt0.min()) / 100.0, [10, 50, 90, 100])],
+        end_us_pct=[float(x) for x in np.percentile((rt1 - rt0.min()) / 100.0, [10, 50, 90, 100])],
     )
 print(json.dumps(out, indent=1))
