@@ -284,7 +284,10 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
 #endif
         // a square problem reaches a free column within N scans; the bound
         // only guarantees termination should the invariants ever break
-        for (int guard = 0; guard < N; ++guard) {
+        // One loop exit per iteration (a free column reached, or the guard);
+        // the exact-tie reduction is the only other branch and is rare.
+        int guard = 0, r4c, jsel;
+        do {
 #ifdef GSM_STAMPS   // diagnostic builds: path iterations
             if (iters) ++*iters;
 #endif
@@ -310,14 +313,13 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
             // (unassigned) or 63 - pos (assigned), larger key winning.
             // Lanes outside `remaining` carry INT_MAX, above every finite key.
             const int kmin = min32_i(key);
-            const uint64_t near = __builtin_amdgcn_ballot_w64(key == kmin) & remm;
-            if (!near) break;
-            int jsel;
+            // (bit 63 is never in `remaining`, N <= 32: an empty `near` —
+            // impossible for finite costs — selects lane 63, whose row4col is
+            // -1, and the sink check below rejects it)
+            const uint64_t near = (__builtin_amdgcn_ballot_w64(key == kmin) & remm) | (1ull << 63);
+            jsel = first_lane(near);
             double m;
-            if (__builtin_expect(!(near & (near - 1)), 1)) {
-                jsel = first_lane(near);
-                m = rl_d(spc, jsel);
-            } else {
+            if (__builtin_expect((near & (near - 1)) != (1ull << 63), 0) && jsel < 63) {
                 m = min32(sel_lanes(near, spc, kInf));
                 const uint64_t cand = __builtin_amdgcn_ballot_w64(spc == m) & remm;
                 jsel = first_lane(cand);
@@ -326,9 +328,11 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
                     const int kb = max32(tkey);
                     jsel = first_lane(__builtin_amdgcn_ballot_w64(tkey == kb));
                 }
+            } else {
+                m = rl_d(spc, jsel);
             }
             minVal = m;
-            const int r4c = __builtin_amdgcn_readlane(row4col, jsel);
+            r4c = __builtin_amdgcn_readlane(row4col, jsel);
             const int at = __builtin_amdgcn_readlane(rpos, jsel);
             remm &= ~(1ull << jsel);
             key = sel_lanes(1ull << jsel, 0x7fffffff, key);
@@ -336,12 +340,9 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
             // remaining[index] = remaining[--n]: the lane at the last position
             // moves to jsel's
             rpos = sel_lanes(__builtin_amdgcn_ballot_w64(rpos == nrem) & remm, at, rpos);
-            if (r4c < 0) {
-                sink = jsel;
-                break;
-            }
             i = r4c;
-        }
+        } while (r4c >= 0 && ++guard < N);
+        if (r4c < 0 && jsel < N) sink = jsel;
 #ifdef GSM_STAMPS
         asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tb_)::"memory");
 #endif

@@ -863,6 +863,21 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     obs_sweep<kN, kNo, kG>(p, s, L, s_pos, s_nf, pm, full, oo, row, cand, ccnt, coinc);
 #endif
     GSM_STAMP(p, wid, 4);
+#if defined(GSM_PAD_SALU) || defined(GSM_PAD_VALU)   // experiment: marginal cost of extra instructions
+    {
+        uint32_t ps = (uint32_t)__builtin_amdgcn_readfirstlane(L.b), pv = (uint32_t)L.lane;
+#pragma unroll
+        for (int k = 0; k < 50; ++k) {
+#ifdef GSM_PAD_SALU
+            asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 3\n\ts_xor_b32 %0, %0, 5\n\ts_add_u32 %0, %0, 7" : "+s"(ps));
+#endif
+#ifdef GSM_PAD_VALU
+            asm volatile("v_add_u32 %0, %0, 1\n\tv_add_u32 %0, %0, 3\n\tv_xor_b32 %0, %0, 5\n\tv_add_u32 %0, %0, 7" : "+v"(pv));
+#endif
+        }
+        asm volatile("" :: "s"(ps), "v"(pv));
+    }
+#endif
 
     // reward / cost callbacks
     float r = 0.0f;
