@@ -249,7 +249,7 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
     } else if (p->path == gsm::kPathSeg) {
         // positions + staged node-feature rows of the wave's G envs
         p->wave_lds_step = align16(8 * p->G * p->E + 28 * p->G * p->E);
-        // one env per wave: + the staged edge list (emit_rows_staged)
+        // one env per wave: + the staged edge list (stage_rows)
         p->wave_lds_emit = align16(p->G == 1 ? 36 * p->E : 8 * p->G * p->E);
     } else {
         // tile: whole-workgroup LDS: positions, velocities, new positions, costs, reductions,

@@ -643,14 +643,17 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
 #endif
         r = -own;
     }
+    // output base pointers read here (kernarg view), not held across the assignment
+    KernargParams &kq = late_params();
+    float2 *const pos_out = kq.pos + eb * Emax;
     float rsum = wave_sum(lane < s.N ? r : 0.0f);
     if (p.shared_reward) {
         r = rsum;
         rsum *= (float)s.N;
     }
     if (lane < Nmax) {
-        p.reward[eb * Nmax + lane] = lane < s.N ? r : 0.0f;
-        p.cost[eb * Nmax + lane] = (float)cnt;
+        kq.reward[eb * Nmax + lane] = lane < s.N ? r : 0.0f;
+        kq.cost[eb * Nmax + lane] = (float)cnt;
     }
     const int csum = wave_sum(cnt);
 
@@ -658,7 +661,7 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
         acc.x += rsum;
         acc.y += (float)csum;
         if (done && p.auto_reset) {
-            if (lane == 0) p.ep_last[b] = acc;
+            if (lane == 0) kq.ep_last[b] = acc;
             relayout();
             // observation of the new layout
             rmask = pair_sweep(&cnt);
@@ -679,7 +682,7 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
         tgt = make_float2(__shfl(slot.x, src), __shfl(slot.y, src));
     }
     if (lane < s.N) {
-        float *nf = p.node_feat + (eb * Emax + lane) * 7;
+        float *nf = kq.node_feat + (eb * Emax + lane) * 7;
         nf[0] = v.x;
         nf[1] = v.y;
         nf[2] = cp.x;
@@ -688,7 +691,7 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
         nf[5] = tgt.y - cp.y;
         if (full_nf) nf[6] = 0.0f;
     }
-    if (lane < Nmax) p.assign[eb * Nmax + lane] = (lane < s.N && s.scn != kScnNav) ? sigma : -1;
+    if (lane < Nmax) kq.assign[eb * Nmax + lane] = (lane < s.N && s.scn != kScnNav) ? sigma : -1;
 
     if (full_nf) {
         // every storage row: positions (padding 0) and the static node rows
@@ -699,13 +702,13 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
         wave_sync();
         for (int q = lane; q < Emax; q += kWave) {
             const float2 pq = s_pos[q];
-            if (full) pos_b[q] = pq;
+            if (full) pos_out[q] = pq;
             if (q < s.N) continue;   // live agent rows written above
             float type;
             if (q < Nmax) type = -1.0f;
             else if (q < Nmax + Tmax) type = q - Nmax < s.T ? 1.0f : -1.0f;
             else type = q - Nmax - Tmax < s.O ? 2.0f : -1.0f;
-            float *nf = p.node_feat + (eb * Emax + q) * 7;
+            float *nf = kq.node_feat + (eb * Emax + q) * 7;
             nf[0] = 0.0f;
             nf[1] = 0.0f;
             nf[2] = pq.x;
@@ -716,24 +719,24 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
         }
     }
     if (full) {
-        if (lane < Nmax) p.vel[eb * Nmax + lane] = lane < s.N ? v : make_float2(0.0f, 0.0f);
+        if (lane < Nmax) kq.vel[eb * Nmax + lane] = lane < s.N ? v : make_float2(0.0f, 0.0f);
     } else if (lane < s.N) {
-        pos_b[lane] = cp;
-        p.vel[eb * Nmax + lane] = v;
+        pos_out[lane] = cp;
+        kq.vel[eb * Nmax + lane] = v;
     }
 
-    if (lane < s.M) p.row_mask[eb * Mmax + lane] = rmask;
+    if (lane < s.M) kq.row_mask[eb * Mmax + lane] = rmask;
     const int edges = wave_sum((int)__popcll(rmask)) + 2 * s.N * s.Tper;
     const bool nonfin = __any(lane < s.N && nonfinite2(cp));
     if (lane == 0) {
-        if (p.degenerate)
-            p.degenerate[b] = (uint8_t)((coinc ? kDegCoincident : 0) | (nonfin ? kDegNonfinite : 0));
-        p.step_count[b] = t;
-        p.episode[b] = ep;
-        p.ep_acc[b] = acc;
-        p.done[b] = done ? 1 : 0;
-        p.edge_count[b] = edges;
-        if (relaid) p.env_shape[b] = s.N | (s.scn << 8);
+        if (kq.degenerate)
+            kq.degenerate[b] = (uint8_t)((coinc ? kDegCoincident : 0) | (nonfin ? kDegNonfinite : 0));
+        kq.step_count[b] = t;
+        kq.episode[b] = ep;
+        kq.ep_acc[b] = acc;
+        kq.done[b] = done ? 1 : 0;
+        kq.edge_count[b] = edges;
+        if (relaid) kq.env_shape[b] = s.N | (s.scn << 8);
     }
 #ifdef GSM_STAMPS
     if (p.stamps && lane == 0) p.stamps[(int64_t)b * 16 + 3] = (uint64_t)(s.N | (s.scn << 8));

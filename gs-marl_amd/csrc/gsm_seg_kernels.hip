@@ -516,10 +516,13 @@ __device__ __forceinline__ void emit_rows(const Shape<kN, kNo> &s, const Lane &L
 // few instructions per set bit of its row, so the row-length imbalance across
 // lanes costs little — then written by all 64 lanes, edge e by lane e mod 64:
 // distances from the staged positions and three coalesced stores per 64 edges.
+// The expansion needs no global offset, so it runs before the workgroup's
+// prefix exchange (block_emit) and fills the wait at its barrier.
+// stage_rows returns the env's edge count, or -1 (nothing staged) when the
+// list exceeds the scratch.
 template <int kN, int kNo>
-__device__ __forceinline__ void emit_rows_staged(const Lane &L, const float2 *s_pos, uint32_t *s_scr,
-                                                 uint64_t mask, int64_t env_off, const EdgeSink &out) {
-    constexpr int N = kN, E = 2 * kN + kNo;
+__device__ __forceinline__ int stage_rows(const Lane &L, uint32_t *s_scr, int scr_cap, uint64_t mask) {
+    constexpr int N = kN;
     static_assert(N <= 31 && kNo <= 32, "agent and obstacle column bits in one word each");
     const int m = L.m;
     const uint64_t mk = L.live ? mask : 0ull;
@@ -528,6 +531,7 @@ __device__ __forceinline__ void emit_rows_staged(const Lane &L, const float2 *s_
     const int incl = wave_scan(c);
     const int a_total = __builtin_amdgcn_readlane(incl, N - 1);
     const int total = __builtin_amdgcn_readlane(incl, 63) + N;
+    if (total > scr_cap) return -1;
     uint32_t *at = s_scr + (incl - c + (m >= N ? N : 0));
     const uint32_t src = (uint32_t)row_entity(m, N);
     for (uint32_t w = lo; w; w &= w - 1) *at++ = src | ((uint32_t)__builtin_ctz(w) << 8);
@@ -537,6 +541,12 @@ __device__ __forceinline__ void emit_rows_staged(const Lane &L, const float2 *s_
     }
     for (uint32_t w = hi; w; w &= w - 1) *at++ = src | ((uint32_t)(2 * N + __builtin_ctz(w)) << 8);
     wave_sync();
+    return total;
+}
+template <int kN, int kNo>
+__device__ __forceinline__ void write_staged(const Lane &L, const float2 *s_pos, const uint32_t *s_scr, int total,
+                                             int64_t env_off, const EdgeSink &out) {
+    constexpr int E = 2 * kN + kNo;
     const int64_t eb = L.b;
     const int32_t g0 = (int32_t)(eb * E);
     const uint32_t wb_lo = __builtin_amdgcn_readfirstlane((uint32_t)env_off);
@@ -549,7 +559,8 @@ __device__ __forceinline__ void emit_rows_staged(const Lane &L, const float2 *s_
         const uint32_t a = w & 0xffu, b = w >> 8;
         const float2 pa = s_pos[a], pb = s_pos[b];
         const float dx = pa.x - pb.x, dy = pa.y - pb.y;
-        const uint32_t byte = (uint32_t)e << 2;
+        uint32_t byte = (uint32_t)e << 2;
+        asm("" : "+v"(byte));   // keeps the stores in SGPR-base + 32-bit-offset form
         *(int32_t *)(isrc + byte) = g0 + (int32_t)a;
         *(int32_t *)(idst + byte) = g0 + (int32_t)b;
         *(float *)(attr + byte) = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
@@ -598,6 +609,15 @@ __device__ __forceinline__ void block_emit(const DevParams &p, const Shape<kN, k
                                            int64_t *edge_ptr, const EdgeSink &out, uint32_t *s_scr,
                                            int scr_cap) {
     const int first = blockIdx.x * kWavesPerBlock * s.G;
+    // one env per wave, compile-time shape: the env's list is staged in LDS
+    // before the prefix exchange (needs only local counts)
+    constexpr bool kStaged = kG == 1 && kN > 0 && kN <= 31 && kNo <= 32;
+    int staged = -1;
+#ifndef GSM_ABL_NO_ROWS
+    if constexpr (kStaged) {
+        if (L.b < p.B) staged = stage_rows<kN, kNo>(L, s_scr, scr_cap, mask);
+    }
+#endif
     const int acc = wave_total(pre.acc);
     const int incl_k = wave_scan(pre.cnt_k);     // envs of this block in order
 #ifdef GSM_ABL_NO_LAGBAR   // timing-only: no workgroup exchange of the prefix
@@ -626,11 +646,12 @@ __device__ __forceinline__ void block_emit(const DevParams &p, const Shape<kN, k
     if (my_cnt < 0)
 #endif
     {
-        if constexpr (kG == 1 && kN > 0 && kN <= 31 && kNo <= 32) {
-            // wave-uniform: the staged path when the env's list fits the scratch
-            // and the outputs (a redirected slot may be smaller than the worst case)
-            if (L.b < p.B && my_cnt <= scr_cap && env_off + my_cnt <= out.cap) {
-                emit_rows_staged<kN, kNo>(L, s_pos, s_scr, mask, env_off, out);
+        if constexpr (kStaged) {
+            // wave-uniform: the staged path when the env's list fit the scratch
+            // and fits the outputs (a redirected slot may be smaller than the
+            // worst case)
+            if (staged >= 0 && env_off + staged <= out.cap) {
+                write_staged<kN, kNo>(L, s_pos, s_scr, staged, env_off, out);
                 return;
             }
         }
@@ -863,21 +884,6 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     obs_sweep<kN, kNo, kG>(p, s, L, s_pos, s_nf, pm, full, oo, row, cand, ccnt, coinc);
 #endif
     GSM_STAMP(p, wid, 4);
-#if defined(GSM_PAD_SALU) || defined(GSM_PAD_VALU)   // experiment: marginal cost of extra instructions
-    {
-        uint32_t ps = (uint32_t)__builtin_amdgcn_readfirstlane(L.b), pv = (uint32_t)L.lane;
-#pragma unroll
-        for (int k = 0; k < 50; ++k) {
-#ifdef GSM_PAD_SALU
-            asm volatile("s_add_u32 %0, %0, 1\n\ts_add_u32 %0, %0, 3\n\ts_xor_b32 %0, %0, 5\n\ts_add_u32 %0, %0, 7" : "+s"(ps));
-#endif
-#ifdef GSM_PAD_VALU
-            asm volatile("v_add_u32 %0, %0, 1\n\tv_add_u32 %0, %0, 3\n\tv_xor_b32 %0, %0, 5\n\tv_add_u32 %0, %0, 7" : "+v"(pv));
-#endif
-        }
-        asm volatile("" :: "s"(ps), "v"(pv));
-    }
-#endif
 
     // reward / cost callbacks
     float r = 0.0f;
