@@ -27,7 +27,7 @@ for c in h c2 c3 c4; do
 done
 cd "$GRAFT_REPO_ROOT"
 for c in h c2 c3 c4 h_driver; do
-  python -c "import json;d=json.load(open('$O/bench_$c.json'));r=d['roofline'];print('$c',d['value'],'us/step',round(d['ms_per_step']*1e3,2),r['kernel'],r['mean_launch_us'],'us frac',r['frac'],'valu',r['valu_frac'],'traffic',r['traffic'],'bounds',d['timed_region']['episode_boundaries'])"
+  python -c "import json;d=json.load(open('$O/bench_$c.json'));r=d['roofline'];print('$c',d['value'],'us/step',round(d['ms_per_step']*1e3,2),r['kernel'],r['mean_launch_us'],'us frac',r['frac'],'valu',r['valu_frac'],'issue',r.get('issue_frac'),'traffic',r['traffic'],'bounds',d['timed_region']['episode_boundaries'])"
 done
 tail -2 $O/bench_gpus2.out
 echo done
