@@ -313,14 +313,14 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
             // (unassigned) or 63 - pos (assigned), larger key winning.
             // Lanes outside `remaining` carry INT_MAX, above every finite key.
             const int kmin = min32_i(key);
-            // (bit 63 is never in `remaining`, N <= 32: an empty `near` —
-            // impossible for finite costs — selects lane 63, whose row4col is
-            // -1, and the sink check below rejects it)
-            const uint64_t near = (__builtin_amdgcn_ballot_w64(key == kmin) & remm) | (1ull << 63);
-            jsel = first_lane(near);
+            // Columns are lanes 0..31 (N <= 32): 32-bit masks keep the test in
+            // SALU. An empty `near` (impossible for finite costs) selects lane
+            // 63, whose row4col is -1, and the sink check below rejects it.
+            const uint32_t near = (uint32_t)(__builtin_amdgcn_ballot_w64(key == kmin) & remm);
+            jsel = near ? __builtin_ctz(near) : 63;
             double m;
-            if (__builtin_expect((near & (near - 1)) != (1ull << 63), 0) && jsel < 63) {
-                m = min32(sel_lanes(near, spc, kInf));
+            if (__builtin_expect((near & (near - 1)) != 0u, 0)) {   // several near: exact f64 minimum
+                m = min32(sel_lanes((uint64_t)near, spc, kInf));
                 const uint64_t cand = __builtin_amdgcn_ballot_w64(spc == m) & remm;
                 jsel = first_lane(cand);
                 if (cand & (cand - 1)) {
