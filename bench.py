@@ -443,13 +443,21 @@ def run_rank(args):
         dist.barrier()
     sync()
     t0 = time.perf_counter()
+    pending = None
     for _ in range(n_chunks):
-        run_steps(chunk, 0)
-        if world > 1:   # the only collective: per-episode metrics (RCCL/xGMI)
+        if world > 1:
+            # the only collective: the episode metrics as of this chunk's start,
+            # SUM-reduced over RCCL/xGMI while the chunk's kernels run (the
+            # collective waits only for the snapshot copy queued before it)
+            if pending is not None:
+                pending.wait()
             metrics.copy_(env.episode_metrics())
-            all_reduce_metrics(metrics)
+            pending = all_reduce_metrics(metrics, async_op=True)
+        run_steps(chunk, 0)
     if rem:
         run_steps(rem, 1)
+    if pending is not None:
+        pending.wait()
     sync()
     if world > 1:
         dist.barrier()

@@ -26,11 +26,17 @@ def shard_config(cfg: EnvConfig, rank: int, world_size: int, envs_per_rank: int 
     return replace(cfg, n_envs=n, env_base=int(cfg.env_base) + rank * n)
 
 
-def all_reduce_metrics(vec: torch.Tensor, group=None) -> torch.Tensor:
-    """SUM-reduce the per-shard metric vector across ranks (in place)."""
+def all_reduce_metrics(vec: torch.Tensor, group=None, async_op: bool = False):
+    """SUM-reduce the per-shard metric vector across ranks (in place). With
+    ``async_op`` the collective is only enqueued (RCCL: on its own stream,
+    after the work already queued on the current one) and the work handle is
+    returned (None without a process group); ``handle.wait()`` orders later
+    work after it. Otherwise returns ``vec``."""
     if dist.is_available() and dist.is_initialized():
-        dist.all_reduce(vec, op=dist.ReduceOp.SUM, group=group)
-    return vec
+        work = dist.all_reduce(vec, op=dist.ReduceOp.SUM, group=group, async_op=async_op)
+        if async_op:
+            return work
+    return None if async_op else vec
 
 
 def max_over_ranks(x: float, device="cpu", group=None) -> float:
