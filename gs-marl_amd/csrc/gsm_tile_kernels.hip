@@ -436,9 +436,13 @@ __device__ __forceinline__ uint32_t *expand_row(const DevParams &p, const uint64
 // e mod 512 — coalesced stores and no row-length imbalance; otherwise each
 // thread writes its runs directly (bounded by the output capacity). s_red:
 // kTileWaves ints.
+// One env's edges (workgroup-wide). The env's global offset is the sum of
+// the threads' `before` partials (edge counts of earlier envs): it is reduced
+// in the same LDS exchange as the row-count scan (one barrier), then returned
+// in *off. s_red: 2 * kTileWaves ints.
 __device__ __forceinline__ void emit_env(const DevParams &p, const EdgeSink &out, const float2 *s_pos,
-                                         const uint64_t *rmask, int64_t off, int *s_red, uint32_t *s_scr,
-                                         int scr_cap, int32_t g0) {
+                                         const uint64_t *rmask, int before, int64_t *off_out, int *s_red,
+                                         uint32_t *s_scr, int scr_cap, int32_t g0) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int E = p.E;
     const int R = (E + kTileBlock - 1) / kTileBlock;
@@ -446,9 +450,14 @@ __device__ __forceinline__ void emit_env(const DevParams &p, const EdgeSink &out
     int mine = 0;
     for (int r = r0; r < r1; ++r) mine += row_edges<false>(p, out, s_pos, rmask, r, 0, g0);
     const int incl = wave_scan(mine);
-    __syncthreads();
+    const int btot = wave_total(before);
     if (lane == 63) s_red[wave] = incl;
+    if (lane == 0) s_red[kTileWaves + wave] = btot;
     __syncthreads();
+    int64_t off = 0;
+#pragma unroll
+    for (int w = 0; w < kTileWaves; ++w) off += s_red[kTileWaves + w];
+    *off_out = off;
     int base = incl - mine, total = 0;
 #pragma unroll
     for (int w = 0; w < kTileWaves; ++w) {
@@ -475,7 +484,6 @@ __device__ __forceinline__ void emit_env(const DevParams &p, const EdgeSink &out
         int64_t o = off + base;
         for (int r = r0; r < r1; ++r) o += row_edges<true>(p, out, s_pos, rmask, r, o, g0);
     }
-    __syncthreads();   // s_red and s_scr are reused by the caller
 }
 
 __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel(DevParams p) {
@@ -700,17 +708,18 @@ __global__ __launch_bounds__(kTileBlock) void gsm_emit_tile_kernel(DevParams p) 
     const int tid = threadIdx.x;
     const int E = p.E;
     float2 *s_pos = (float2 *)smem;
-    int *s_red = (int *)(s_pos + E);          // [kTileWaves]
-    uint32_t *s_scr = (uint32_t *)(s_red + kTileWaves);   // staged edge words
-    const int scr_cap = (p.wave_lds_emit - 8 * E - 4 * kTileWaves) / 4;
+    int *s_red = (int *)(s_pos + E);          // [2 * kTileWaves]
+    uint32_t *s_scr = (uint32_t *)(s_red + 2 * kTileWaves);   // staged edge words
+    const int scr_cap = (p.wave_lds_emit - 8 * E - 8 * kTileWaves) / 4;
     const int64_t eb = b;
-    // global offset: edges of envs [0, b)  (host keeps totals < 2^31)
+    // global offset: edges of envs [0, b)  (host keeps totals < 2^31), reduced
+    // inside emit_env with the row-count scan
     int before = 0;
     for (int k = tid; k < b; k += kTileBlock) before += p.edge_count[k];
     for (int e = tid; e < E; e += kTileBlock) s_pos[e] = p.pos[eb * E + e];
-    const int64_t off = tile_sum(before, s_red);
-    emit_env(p, EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity}, s_pos, p.row_mask + eb * p.M * p.W, off,
-             s_red, s_scr, scr_cap, (int32_t)(eb * E));
+    int64_t off;   // (emit_env's exchange barrier also publishes the staged positions)
+    emit_env(p, EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity}, s_pos, p.row_mask + eb * p.M * p.W, before,
+             &off, s_red, s_scr, scr_cap, (int32_t)(eb * E));
     if (tid == 0) {
         p.edge_ptr[b] = off;
         if (b == p.B - 1) p.edge_ptr[p.B] = off + p.edge_count[b];
