@@ -256,7 +256,7 @@ void derive(const gsm_config *c, gsm::DevParams *p) {
         // the two degenerate-state flags;
         // + the symmetric sweep's column pairs, agent-row words and obstacle-row
         // agent bits when they fit in 32 KB (gsm_tile_kernels.hip: obs_sweep_sym)
-        p->wave_lds_step = align16(8 * p->E + 8 * N + 8 * N + 4 * N + 8 * (gsm::kTileBlock / gsm::kWave) + 8);
+        p->wave_lds_step = align16(8 * p->E + 8 * N + 8 * N + 4 * N + 20 * (gsm::kTileBlock / gsm::kWave) + 8);
         const int sym = 16 * ((N + 1) / 2) + 16 * N * p->W + 8 * No * p->W + 16;
         p->tile_sym = sym <= 32768;
         if (p->tile_sym) p->wave_lds_step += sym;

@@ -428,18 +428,16 @@ __device__ __forceinline__ uint32_t *expand_row(const DevParams &p, const uint64
     return at;
 }
 
-// Env b's edges at global offset `off` (workgroup-wide: barriers): each
-// thread takes a contiguous run of rows, counts them from the mask words, a
-// workgroup scan gives the run offsets. When the env's edges fit the LDS
-// scratch s_scr (scr_cap words) and the outputs, the runs are first expanded
-// into s_scr in CSR order and then written by every thread, edge e by thread
-// e mod 512 — coalesced stores and no row-length imbalance; otherwise each
-// thread writes its runs directly (bounded by the output capacity). s_red:
-// kTileWaves ints.
-// One env's edges (workgroup-wide). The env's global offset is the sum of
-// the threads' `before` partials (edge counts of earlier envs): it is reduced
-// in the same LDS exchange as the row-count scan (one barrier), then returned
-// in *off. s_red: 2 * kTileWaves ints.
+// Env b's edges (workgroup-wide: barriers): each thread takes a contiguous
+// run of rows, counts them from the mask words, a workgroup scan gives the
+// run offsets. The env's global offset `off` is the sum of the threads'
+// `before` partials (edge counts of earlier envs), reduced in the same LDS
+// exchange as the scan (one barrier) and returned in *off_out. When the env's
+// edges fit the LDS scratch s_scr (scr_cap words) and the outputs, the runs
+// are first expanded into s_scr in CSR order and then written by every
+// thread, edge e by thread e mod 512 — coalesced stores and no row-length
+// imbalance; otherwise each thread writes its runs directly (bounded by the
+// output capacity). s_red: 2 * kTileWaves ints.
 __device__ __forceinline__ void emit_env(const DevParams &p, const EdgeSink &out, const float2 *s_pos,
                                          const uint64_t *rmask, int before, int64_t *off_out, int *s_red,
                                          uint32_t *s_scr, int scr_cap, int32_t g0) {
@@ -495,13 +493,13 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
     float2 *s_vel = s_pos + E;                // [N]
     float2 *s_np = s_vel + N;                 // [N] integrated agent positions
     int *s_cost = (int *)(s_np + N);          // [N]
-    int *s_ired = s_cost + N;                 // [kTileWaves]
-    float *s_fred = (float *)(s_ired + kTileWaves);
+    int *s_ired = s_cost + N;                 // [4 * kTileWaves] reduction slots
+    float *s_fred = (float *)(s_ired + 4 * kTileWaves);
     int *s_deg = (int *)(s_fred + kTileWaves);   // [2] coincident pair (unsymmetric sweep), non-finite agent
     // symmetric sweep scratch (p.tile_sym), 16-byte aligned after the above
     TileSymLds sym;
     {
-        unsigned char *q = smem + ((8 * E + 8 * N + 8 * N + 4 * N + 8 * kTileWaves + 8 + 15) & ~15);
+        unsigned char *q = smem + ((8 * E + 8 * N + 8 * N + 4 * N + 20 * kTileWaves + 8 + 15) & ~15);
         sym.xy = (float *)q;
         q += 16 * ((N + 1) / 2);
         sym.arow = (uint64_t *)q;
@@ -612,25 +610,59 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
     int pairs = 0;
     for (int i = tid; i < N; i += kTileBlock) s_cost[i] = 0;
 #endif
-    // reward callback: -|p_i - g_i|
+    // reward and cost callbacks, episode accounting. The workgroup sums of
+    // reward, collisions, directed radius pairs and the non-finite flag share
+    // one LDS exchange (an auto-reset, rare, re-sweeps and exchanges again).
+    auto nonfinite_part = [&]() {
+        int bad = 0;
+        if (p.degenerate)
+            for (int i = tid; i < N; i += kTileBlock) bad |= nonfinite2(s_pos[i]) ? 1 : 0;
+        return bad;
+    };
     float rpart = 0.0f;
     for (int i = tid; i < N; i += kTileBlock) {
         const float2 a = s_pos[i], g = s_pos[N + i];
         const float dx = a.x - g.x, dy = a.y - g.y;
         rpart += -sqrtf(dx * dx + dy * dy);
     }
-    float rsum = tile_sum(rpart, s_fred);       // (its barriers also publish s_cost)
-    int csum = 0;
+    __syncthreads();   // s_cost from the sweep; the exchange slots are free
+    int cpart = 0;
     for (int i = tid; i < N; i += kTileBlock) {
         const int cnt = s_cost[i];
         p.cost[eb * N + i] = (float)cnt;
-        csum += cnt;
-        const float2 a = s_pos[i], g = s_pos[N + i];
-        const float dx = a.x - g.x, dy = a.y - g.y;
-        p.reward[eb * N + i] = p.shared_reward ? rsum : -sqrtf(dx * dx + dy * dy);
+        cpart += cnt;
+        if (!p.shared_reward) {
+            const float2 a = s_pos[i], g = s_pos[N + i];
+            const float dx = a.x - g.x, dy = a.y - g.y;
+            p.reward[eb * N + i] = -sqrtf(dx * dx + dy * dy);
+        }
     }
-    csum = tile_sum(csum, s_ired);
-    if (p.shared_reward) rsum *= (float)N;
+    {
+        const float rw = wave_total(rpart);
+        const int cw = wave_total(cpart), pw = wave_total(pairs), bw = wave_total(nonfinite_part());
+        if ((tid & 63) == 0) {
+            const int w = tid >> 6;
+            s_fred[w] = rw;
+            s_ired[w] = cw;
+            s_ired[kTileWaves + w] = pw;
+            s_ired[2 * kTileWaves + w] = bw;
+        }
+    }
+    __syncthreads();
+    float rsum = 0.0f;
+    int csum = 0, bad = 0;
+    pairs = 0;
+#pragma unroll
+    for (int w = 0; w < kTileWaves; ++w) {
+        rsum += s_fred[w];
+        csum += s_ired[w];
+        pairs += s_ired[kTileWaves + w];
+        bad |= s_ired[2 * kTileWaves + w];
+    }
+    if (p.shared_reward) {
+        for (int i = tid; i < N; i += kTileBlock) p.reward[eb * N + i] = rsum;
+        rsum *= (float)N;
+    }
 
     if (p.mode == kModeStep) {
         acc.x += rsum;
@@ -640,12 +672,10 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
             relayout();
             pairs = p.tile_sym ? obs_sweep_sym(p, s_pos, sym, s_cost, eb, false)
                                : obs_sweep_any(p, s_pos, s_cost, eb, false, s_deg);
+            pairs = tile_sum(pairs, s_ired);
+            bad = tile_sum(nonfinite_part(), s_ired + 3 * kTileWaves);
         }
     }
-    if (p.degenerate)
-        for (int i = tid; i < N; i += kTileBlock)
-            if (nonfinite2(s_pos[i])) s_deg[1] = 1;
-    pairs = tile_sum(pairs, s_ired);   // (its barriers also publish s_deg)
 
     // node features [E][7] = [vx vy px py gx-px gy-py type]: agent rows every
     // step (one thread per row), goal/obstacle rows only on layout change
@@ -697,7 +727,7 @@ skip_nf:
         p.block_edge_sum[b] = edges;
         if (p.degenerate) {
             const int co = p.tile_sym ? *sym.flag : s_deg[0];
-            p.degenerate[b] = (uint8_t)((co ? kDegCoincident : 0) | (s_deg[1] ? kDegNonfinite : 0));
+            p.degenerate[b] = (uint8_t)((co ? kDegCoincident : 0) | (bad ? kDegNonfinite : 0));
         }
     }
 }
