@@ -18,11 +18,11 @@ constexpr int kTileEmitScr = 6144;   // tile emitter: staged edge words per env 
 constexpr int kRaggedMaxAgents = 32;                                  // = GSM_RAGGED_MAX_AGENTS
 constexpr int kRaggedTable = kRaggedMaxAgents * (kRaggedMaxAgents + 1) / 2;   // rows n = 1..32
 // ragged assignment scratch per wave (gsm_ragged_kernels.hip LsaLds): cost
-// matrix rows (a multiple of 8) at an odd stride, column duals, column -> row
+// matrix rows (a multiple of 8) at an odd stride, column and row duals, column -> row
 __host__ __device__ constexpr int lsa_stride(int nmax) { return nmax | 1; }
 __host__ __device__ constexpr int lsa_cost_bytes(int nmax) { return 4 * ((nmax + 7) & ~7) * lsa_stride(nmax); }
 __host__ __device__ constexpr int lsa_lds_bytes(int nmax) {
-    return ((lsa_cost_bytes(nmax) + 15) & ~15) + 8 * kRaggedMaxAgents + 4 * kRaggedMaxAgents;
+    return ((lsa_cost_bytes(nmax) + 15) & ~15) + 16 * kRaggedMaxAgents + 4 * kRaggedMaxAgents;
 }
 #ifndef GSM_SEG_GMAX   // cap on envs per wave (C2, 3 x 4096: G = 4 runs 6.0 us per step against 6.9 at G = 10)
 #define GSM_SEG_GMAX 4

@@ -201,14 +201,16 @@ struct LsaWarm {
 // 32 distinct banks), the column duals, and a column -> row scratch.
 struct LsaLds {
     float *cost;   // [roundup8(N_max)][S]
-    double *v;     // [32]
+    double *v;     // [32] column duals
+    double *u;     // [32] row duals
     int *keep;     // [32]
     int S;
 };
 __device__ __forceinline__ LsaLds lsa_lds(unsigned char *lds, int nmax) {
     const int S = lsa_stride(nmax);
     const int cb = (lsa_cost_bytes(nmax) + 15) & ~15;
-    return LsaLds{(float *)lds, (double *)(lds + cb), (int *)(lds + cb + 8 * kRaggedMaxAgents), S};
+    return LsaLds{(float *)lds, (double *)(lds + cb), (double *)(lds + cb + 8 * kRaggedMaxAgents),
+                  (int *)(lds + cb + 16 * kRaggedMaxAgents), S};
 }
 
 __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &sl, float *own, LsaWarm w,
@@ -387,6 +389,7 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
         if (col) {
             const float *crow = s_cost + lane * S;
             const int ci = col4row;
+#pragma unroll 4
             for (int j = 0; j < N; ++j) {
                 const double r = (double)crow[j] - u - sl.v[j];
                 good &= j == ci ? fabs(r) <= 1e-11 : r >= -1e-11;
@@ -432,24 +435,64 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
                 sl.keep[lane] = -1;
             }
             wave_sync();
-            double m0 = kInf, m1 = kInf, rc = kInf;
+            // lane i: u_i = min_j (C[i][j] - v_j) and rc = C[i][c0_i] - v_c0
+            double rc = kInf;
+            auto row_pass = [&]() -> double {
+                double m = kInf;
+                if (col) {
+                    const float *crow = s_cost + lane * S;
+                    // chunks of 8 columns: every LDS read of a chunk is issued
+                    // before the first use (one wait per chunk); columns past
+                    // N read scratch and are masked
+                    for (int j0 = 0; j0 < N; j0 += 8) {
+                        float cr[8];
+                        double vj[8];
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            cr[k] = crow[j0 + k];
+                            vj[k] = sl.v[j0 + k];
+                        }
+#pragma unroll
+                        for (int k = 0; k < 8; ++k) {
+                            const double r = (double)cr[k] - vj[k];
+                            m = (j0 + k < N && r < m) ? r : m;
+                        }
+                    }
+                    // the previous column's reduced cost, the same expression as in the scan
+                    rc = (c0 >= 0 && c0 < N) ? (double)crow[c0] - sl.v[c0] : kInf;
+                }
+                return m;
+            };
+            double m = row_pass();
+            // one column reduction (Jonker-Volgenant's): raise each v_j to its
+            // column minimum of C[i][j] - u_i (duals stay feasible), then the
+            // row minima again. Fewer rows lose their previous column: 12.2 ->
+            // 8.9 of 24 in a polygon simulation (oracle/lsa_ref.py duals,
+            // random actions); further rounds keep 8.9.
+            if (lane < kRaggedMaxAgents) sl.u[lane] = col ? m : 0.0;
+            wave_sync();
             if (col) {
-                const float *crow = s_cost + lane * S;
-                int j = 0;
-                for (; j + 1 < N; j += 2) {
-                    const double r0 = (double)crow[j] - sl.v[j];
-                    const double r1 = (double)crow[j + 1] - sl.v[j + 1];
-                    m0 = fmin(m0, r0);
-                    m1 = fmin(m1, r1);
-                    rc = j == c0 ? r0 : (j + 1 == c0 ? r1 : rc);
+                double cm = kInf;
+                for (int i0 = 0; i0 < N; i0 += 8) {   // chunks of 8 rows, reads first
+                    float cc[8];
+                    double ui[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        cc[k] = s_cost[(i0 + k) * S + lane];
+                        ui[k] = sl.u[i0 + k];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const double r = (double)cc[k] - ui[k];
+                        cm = (i0 + k < N && r < cm) ? r : cm;
+                    }
                 }
-                if (j < N) {
-                    const double r0 = (double)crow[j] - sl.v[j];
-                    m0 = fmin(m0, r0);
-                    rc = j == c0 ? r0 : rc;
-                }
+                v = cm;
             }
-            const double m = fmin(m0, m1);
+            wave_sync();
+            if (lane < kRaggedMaxAgents) sl.v[lane] = v;
+            wave_sync();
+            m = row_pass();
             u = col ? m : 0.0;
             // a row keeps its previous column when that column attains its
             // minimum (c0 is a matching, so no column is claimed twice; a
