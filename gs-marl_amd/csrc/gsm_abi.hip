@@ -36,7 +36,9 @@ struct gsm_handle {
         int steps = 0;
         int kern = 0;
         bool each = false;
+        uint64_t *gran = nullptr;     // fused rollout: [K][n_blocks] edge-sum granules
     } slots[GSM_GRAPH_SLOTS];
+    uint32_t *roll_status = nullptr;  // fused rollout: a bounded wait gave up (sticky until read)
 };
 
 namespace {
@@ -344,6 +346,8 @@ void drop_slot(gsm_handle::Slot &s) {
     if (s.exec) (void)hipGraphExecDestroy(s.exec);
     if (s.graph) (void)hipGraphDestroy(s.graph);
     for (hipEvent_t ev : s.events) (void)hipEventDestroy(ev);
+    if (s.gran) (void)hipFree(s.gran);
+    s.gran = nullptr;
     s.exec = nullptr;
     s.graph = nullptr;
     s.events.clear();
@@ -478,6 +482,8 @@ int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream) {
 
 static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_t stride, int32_t n_actions,
                         int32_t n_steps, int action_fmt, int flags, const gsm_outputs *per_step);
+static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_t stride, int32_t n_actions,
+                        int32_t n_steps, int action_fmt, int flags);
 
 int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t stride,
                       int32_t n_actions, int32_t n_steps, int action_fmt, int flags) {
@@ -490,11 +496,156 @@ int gsm_graph_capture_into(gsm_handle *h, int32_t slot, const void *actions, int
     return capture_impl(h, slot, actions, stride, n_actions, n_steps, action_fmt, 0, per_step);
 }
 
+// Fused rollout graph (GSM_GRAPH_ROLL): step_0, a zeroing memset of the
+// granules, ONE gsm_roll_seg_kernel launch for steps 1 .. T-1 (it emits steps
+// 0 .. T-2), emit_{T-1}. Every output equals the lagged chain's.
+static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_t stride, int32_t n_actions,
+                        int32_t n_steps, int action_fmt, int flags) {
+    if (flags & ~(GSM_GRAPH_ROLL | GSM_GRAPH_TIME_ENDS))
+        return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL combines with GSM_GRAPH_TIME_ENDS only");
+    if (!actions || n_actions < 1 || stride < 0) return fail(h, GSM_EINVAL, "bad capture arguments");
+    if (n_steps < 2) return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL needs n_steps >= 2");
+    if (action_fmt < GSM_ACT_ONEHOT || action_fmt > GSM_ACT_CONT) return fail(h, GSM_EINVAL, "bad action_fmt");
+    gsm::DevParams p = h->dp;
+    p.mode = GSM_MODE_STEP;
+    p.action_fmt = action_fmt;
+    p.env_mask = nullptr;
+    p.reseed = 0;
+    const void *roll_fn = gsm::roll_seg_kernel_fn(p);
+    if (!roll_fn) return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: no fused rollout kernel for this config "
+                                             "(segmented path, one env per wave, compiled shape)");
+    const int nb = gsm::step_grid_blocks(p);
+    const size_t roll_lds = gsm::roll_kernel_lds(p);
+    // every workgroup resident at once (one residency round; a workgroup only
+    // waits on lower-numbered ones, so this is for speed, not for progress)
+    int dev = 0, per_cu = 0, n_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess)
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, roll_fn, gsm::block_threads(p), roll_lds);
+    if (e != hipSuccess) return hip_fail(h, e, "occupancy query");
+    if ((int64_t)per_cu * n_cu < nb)
+        return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: the batch exceeds one residency round of the rollout kernel");
+    gsm_handle::Slot &sl = h->slots[slot];
+    drop_slot(sl);
+    if (!h->bsum_alt) {
+        e = hipMalloc(&h->bsum_alt, (size_t)h->sz.n_blocks * sizeof(int32_t) + 16);
+        if (e != hipSuccess) { h->bsum_alt = nullptr; return hip_fail(h, e, "hipMalloc (edge-sum buffer)"); }
+    }
+    if (!h->roll_status) {
+        e = hipMalloc(&h->roll_status, 16);
+        if (e == hipSuccess) e = hipMemset(h->roll_status, 0, 16);
+        if (e != hipSuccess) { h->roll_status = nullptr; return hip_fail(h, e, "hipMalloc (rollout status)"); }
+    }
+    if (!h->cap_stream) {
+        e = hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking);
+        if (e != hipSuccess) return hip_fail(h, e, "hipStreamCreate");
+    }
+    const int K = n_steps - 1;
+    const size_t gran_bytes = (size_t)K * nb * sizeof(uint64_t);   // a multiple of 16 (nb even) or padded
+    const size_t gran_alloc = (gran_bytes + 15) & ~(size_t)15;
+    e = hipMalloc(&sl.gran, gran_alloc);
+    if (e != hipSuccess) { sl.gran = nullptr; return hip_fail(h, e, "hipMalloc (rollout granules)"); }
+    const bool ends = (flags & GSM_GRAPH_TIME_ENDS) != 0;
+    sl.events.resize(ends ? 2 : 0, nullptr);
+    for (auto &ev : sl.events) {
+        e = hipEventCreate(&ev);
+        if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipEventCreate"); }
+    }
+    e = hipGraphCreate(&sl.graph, 0);
+    if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipGraphCreate"); }
+    hipGraphNode_t prev = nullptr;
+    auto add_kernel = [&](const void *fn, const gsm::DevParams &kp_params, int grid, size_t lds) -> hipError_t {
+        hipKernelNodeParams kp = {};
+        gsm::DevParams q = kp_params;
+        void *args[] = {&q};
+        kp.func = const_cast<void *>(fn);
+        kp.gridDim = dim3(grid);
+        kp.blockDim = dim3(gsm::block_threads(q));
+        kp.sharedMemBytes = (unsigned)lds;
+        kp.kernelParams = args;
+        kp.extra = nullptr;
+        hipGraphNode_t n;
+        const hipError_t r = hipGraphAddKernelNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0, &kp);
+        if (r == hipSuccess) prev = n;
+        return r;
+    };
+    auto add_event = [&](hipEvent_t ev) -> hipError_t {
+        hipGraphNode_t n;
+        const hipError_t r = hipGraphAddEventRecordNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0, ev);
+        if (r == hipSuccess) prev = n;
+        return r;
+    };
+    const char *what = "step kernel node";
+    // step 0: the plain step kernel, writing its edge sums to the second half
+    gsm::DevParams p0 = p;
+    p0.actions = actions;
+    p0.block_edge_sum = h->bsum_alt;
+    e = add_kernel(gsm::step_kernel_fn(p0), p0, nb, gsm::step_kernel_lds(p0));
+    if (e == hipSuccess) {
+        what = "memset node";
+        hipMemsetParams mp = {};
+        mp.dst = sl.gran;
+        mp.elementSize = 4;
+        mp.width = gran_alloc / 4;
+        mp.height = 1;
+        mp.pitch = gran_alloc;
+        mp.value = 0;
+        hipGraphNode_t n;
+        e = hipGraphAddMemsetNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0, &mp);
+        if (e == hipSuccess) prev = n;
+    }
+    if (e == hipSuccess && ends) { what = "event node"; e = add_event(sl.events[0]); }
+    // steps 1 .. T-1 in one launch; its final sums go to the bound half
+    gsm::DevParams pr = p;
+    pr.actions = (const char *)actions + (int64_t)(1 % n_actions) * stride;
+    pr.block_edge_sum = h->dp.block_edge_sum;
+    pr.lag = gsm::DevParams::Lag{h->bsum_alt, p.edge_count, p.edge_ptr, p.edge_index, p.edge_attr,
+                                 p.edge_capacity};
+    pr.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 1, K, 0, sl.gran, h->roll_status};
+    if (e == hipSuccess) { what = "rollout kernel node"; e = add_kernel(roll_fn, pr, nb, roll_lds); }
+    if (e == hipSuccess && ends) { what = "event node"; e = add_event(sl.events[1]); }
+    if (e == hipSuccess) {
+        what = "emit kernel node";
+        e = add_kernel(gsm::emit_kernel_fn(pr), pr, gsm::grid_blocks(pr), gsm::emit_kernel_lds(pr));
+    }
+    if (e != hipSuccess) {
+        drop_slot(sl);
+        char where[96];
+        snprintf(where, sizeof where, "rollout graph build (%s)", what);
+        return hip_fail(h, e, where);
+    }
+    e = hipGraphInstantiate(&sl.exec, sl.graph, nullptr, nullptr, 0);
+    if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipGraphInstantiate"); }
+    e = hipGraphUpload(sl.exec, h->cap_stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->cap_stream);
+    if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipGraphUpload"); }
+    // timing (TIME_ENDS): the events bracket the rollout kernel alone, so
+    // gsm_graph_kernel_ms reports its time per step
+    sl.each = false;
+    sl.kern = GSM_GRAPH_STEP;
+    sl.steps = ends ? K : n_steps;
+    return GSM_OK;
+}
+
+int gsm_graph_roll_status(gsm_handle *h, int32_t *gave_up) {
+    if (!h || !gave_up) return fail(h, GSM_EINVAL, "NULL argument");
+    *gave_up = 0;
+    if (!h->roll_status) return GSM_OK;
+    uint32_t v = 0;
+    hipError_t e = hipMemcpy(&v, h->roll_status, sizeof v, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && v) e = hipMemset(h->roll_status, 0, 16);
+    if (e != hipSuccess) return hip_fail(h, e, "rollout status read");
+    *gave_up = v ? 1 : 0;
+    return GSM_OK;
+}
+
 static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_t stride, int32_t n_actions,
                         int32_t n_steps, int action_fmt, int flags, const gsm_outputs *per_step) {
     if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
     if (!h->bound) return fail(h, GSM_ESTATE, "gsm_bind has not been called");
     if (bad_slot(slot)) return fail(h, GSM_EINVAL, "bad graph slot");
+    if (flags & GSM_GRAPH_ROLL) return capture_roll(h, slot, actions, stride, n_actions, n_steps, action_fmt, flags);
     int kern = flags & (GSM_GRAPH_STEP | GSM_GRAPH_EMIT);
     if (!kern) kern = GSM_GRAPH_STEP | GSM_GRAPH_EMIT;
     const bool each = (flags & GSM_GRAPH_TIME_EACH) != 0, ends = (flags & GSM_GRAPH_TIME_ENDS) != 0;
@@ -714,6 +865,7 @@ int gsm_destroy(gsm_handle *h) {
     drop_graph(h);
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->bsum_alt) (void)hipFree(h->bsum_alt);
+    if (h->roll_status) (void)hipFree(h->roll_status);
     if (h->order_copied) (void)hipEventSynchronize(h->order_copied);
     if (h->block_order) (void)hipFree(h->block_order);
     if (h->order_host) (void)hipHostFree(h->order_host);

@@ -86,6 +86,20 @@ struct DevParams {
         float *edge_attr;
         int64_t cap;
     } lag;
+    // Fused rollout (segmented path, one env per wave, graph chains): K
+    // consecutive steps in one launch (gsm_roll_seg_kernel). Iteration k runs
+    // step t_first + k with the actions at actions + ((t_first + k) %
+    // n_actions) * stride and emits the previous step's edges into p.lag's
+    // outputs; the CSR prefix of step t crosses workgroups through `gran`
+    // ({tag = k + 1, workgroup edge sum} 8-byte granules, [K][grid], zeroed
+    // before every launch). `status` is set when a bounded wait gave up.
+    struct Roll {
+        const char *actions;
+        int64_t stride;
+        int32_t n_actions, t_first, K, pad;
+        uint64_t *gran;
+        uint32_t *status;
+    } roll;
 };
 
 // where an emission writes its edges
@@ -110,6 +124,10 @@ const void *step_seg_kernel_fn(const DevParams &p);
 const void *lag_step_kernel_fn(const DevParams &p);
 const void *lag_step_seg_kernel_fn(const DevParams &p);
 const void *emit_seg_kernel_fn(const DevParams &p);
+// fused K-step rollout kernel (nullptr where the config has none: G > 1,
+// runtime shapes, other families) and its LDS bytes
+const void *roll_seg_kernel_fn(const DevParams &p);
+size_t roll_kernel_lds(const DevParams &p);
 const void *step_ragged_kernel_fn();
 const void *step_tile_kernel_fn();
 const void *emit_tile_kernel_fn();

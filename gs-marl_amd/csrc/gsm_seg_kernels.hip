@@ -1099,10 +1099,348 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
     GSM_RSTAMP(p, wid, 9);
 }
 
+// ---------------------------------------------------------------------------
+// Fused rollout: K consecutive steps of a graph chain in ONE launch (one env
+// per wave, compile-time shape). Each wave keeps its env's state
+// on chip across the steps — positions in LDS, velocity / contact candidates /
+// row masks in registers, counters in SGPRs — so a step issues no state loads,
+// and the launch boundary between steps (≈5.5 µs of fixed latency per launch
+// at any batch) is paid once per K steps.
+//
+// Iteration k (step t = t_first + k): physics, observation sweep, reward /
+// cost, auto-reset and every store of step t exactly as gsm_step_seg_kernel
+// (same operations in the same order: bit-identical outputs); the
+// workgroup's edge sum of step t is published as an 8-byte {tag = k + 1, sum}
+// granule (one relaxed agent-scope store: write-through, no fence); then the
+// edges of step t - 1 are emitted from the positions and row masks kept from
+// the previous iteration, at the CSR offset = the sum of the preceding
+// workgroups' granules of iteration k - 1 (relaxed agent-scope loads, every
+// tag checked). Those granules were published one iteration earlier, so the
+// wait is normally already satisfied. A workgroup waits only on workgroups
+// with smaller index (dispatched before it), so the chain always progresses;
+// every wait is bounded (kRollSpinTicks, then p.roll.status is set and the
+// launch drains). Step t_first - 1's edges are emitted first (prefix from the
+// previous launch's sums, as the lagged kernel); the last step's edges are
+// left to the emit launch that ends the graph.
+#ifndef GSM_ROLL_ATTR   // all 8 waves per SIMD resident (2048 workgroups at 8192 envs: one residency round)
+#define GSM_ROLL_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
+#endif
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+constexpr uint64_t kRollSpinTicks = 20000000ull;   // s_memrealtime ticks (100 MHz): 0.2 s
+
+// one granule, polled until its tag matches (cold path)
+__device__ __forceinline__ uint64_t roll_wait(const uint64_t *g, uint32_t tag, uint32_t *status) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const uint64_t x = __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(x >> 32) == tag) return x;
+        if (__hip_atomic_load((gu32 *)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+            __builtin_amdgcn_s_memrealtime() - t0 > kRollSpinTicks) {
+            __hip_atomic_store((gu32 *)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return (uint64_t)tag << 32;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// this thread's part of the sum of the granules of workgroups [0, blockIdx.x)
+// (loads at clamped addresses first, tags checked afterwards)
+__device__ __forceinline__ int roll_prefix_part(const uint64_t *gran_k, uint32_t tag, uint32_t *status) {
+    const int w = (int)blockIdx.x, tid = (int)threadIdx.x;
+    int acc = 0;
+    for (int base = 0; base < w; base += 8 * kBlock) {
+        uint64_t x[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int i = base + tid + j * kBlock;
+            x[j] = __hip_atomic_load((const gu64 *)(gran_k + (i < w ? i : w - 1)), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int i = base + tid + j * kBlock;
+            if (i < w) {
+                if ((uint32_t)(x[j] >> 32) != tag) x[j] = roll_wait(gran_k + i, tag, status);
+                acc += (int)(uint32_t)x[j];
+            }
+        }
+    }
+    return acc;
+}
+
+// a lane's action of the given step row, as loaded (decoded by roll_force)
+template <int kN, int kFmt, typename Params>   // DevParams or its kernarg view
+__device__ __forceinline__ float4 roll_action_load(const Params &p, int row, int64_t eb, uint32_t ma) {
+    const char *base = p.roll.actions + (int64_t)row * p.roll.stride;
+    const int64_t ai = eb * kN + ma;
+    if constexpr (kFmt == 0) {
+        const float *q = (const float *)base + ai * 5;
+        return make_float4(q[1], q[2], q[3], q[4]);
+    } else if constexpr (kFmt == 1) {
+        return make_float4(__int_as_float(((const int32_t *)base)[ai]), 0.0f, 0.0f, 0.0f);
+    } else {
+        const float2 a = ((const float2 *)base)[ai];
+        return make_float4(a.x, a.y, 0.0f, 0.0f);
+    }
+}
+template <int kFmt, typename Params>
+__device__ __forceinline__ float2 roll_force(const Params &p, float4 a, bool agent) {
+    float ux, uy;
+    if constexpr (kFmt == 0) {
+        ux = a.x - a.y;
+        uy = a.z - a.w;
+    } else if constexpr (kFmt == 1) {
+        const int k = __float_as_int(a.x);
+        ux = (float)(k == 1) - (float)(k == 2);
+        uy = (float)(k == 3) - (float)(k == 4);
+    } else {
+        ux = a.x;
+        uy = a.y;
+    }
+    return agent ? make_float2(ux * p.sens, uy * p.sens) : make_float2(0.0f, 0.0f);
+}
+
+template <int kN, int kNo, int kFmt>
+__global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevParams p) {
+    static_assert(envs_per_wave<kN, kNo>() == 1 && kFmt >= 0, "one env per wave, compile-time shape");
+    constexpr int N = kN, M = kN + kNo, E = 2 * kN + kNo;
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const Shape<kN, kNo> s(p);
+    const Lane L0 = seg_lane(p, s);
+    const int wave = L0.wave;
+    const int wstride = p.wave_lds_step + 8 * E;            // + the previous step's positions
+    unsigned char *wave_lds = smem + wave * wstride;
+    float2 *s_pos = (float2 *)wave_lds;
+    float *s_nf = (float *)(s_pos + E);
+    float2 *s_prev = (float2 *)(wave_lds + p.wave_lds_step);
+    int *s_bc = (int *)(smem + kWavesPerBlock * wstride);   // [2][waves]: per-env edge counts by parity
+    int *s_red = s_bc + 2 * kWavesPerBlock;
+    const int scr_cap = (p.wave_lds_step - 8 * E) / 4;
+    const bool wave_live = L0.b < p.B;
+    const int64_t eb = wave_live ? L0.b : 0;
+    
+    // ---- step t_first - 1's state and step t_first's actions (p.actions), the
+    // previous launch's edge sums; its edges first, as the lagged kernel
+    SegIn in = seg_load<kN, kNo, kFmt, true>(p, s, L0);
+    const BlockPrefix pre0 = block_prefix_loads(p.lag.block_sum, p.lag.edge_count, p.B, 1, p.pos);
+    seg_load_finish<kN, kNo, kFmt, true>(p, L0, in);
+    int t = in.t, ep = in.ep;
+    float2 acc = in.acc, v = in.v, u = in.u;
+    uint64_t cand_prev = in.cand_prev, oo = in.oo;
+    if (wave_live) {
+        if (L0.lane < E) s_pos[L0.lane] = in.x0;
+        if (L0.lane + kWave < E) s_pos[L0.lane + kWave] = in.x1;
+    }
+    wave_sync();
+    {
+        KernargParams &q = late_params();
+        block_emit<kN, kNo, 1>(p, s, L0, s_pos, oo, pre0, s_red, q.lag.edge_ptr,
+                               EdgeSink{q.lag.edge_index, q.lag.edge_attr, q.lag.cap}, (uint32_t *)s_nf, scr_cap);
+    }
+    wave_sync();
+
+    const int K = p.roll.K, n_act = p.roll.n_actions;
+    int arow = p.roll.t_first % n_act;                      // action row of the current step
+    for (int k = 0; k < K; ++k) {
+        // lane-derived values re-formed every iteration (an asm barrier): held
+        // across the loop they would pin their hoisted addresses in VGPRs
+        Lane L = L0;
+        asm volatile("" : "+v"(L.lane), "+v"(L.m));
+        const int m = L.m;
+        const uint32_t um = (uint32_t)m, ma = L.lane < N ? (uint32_t)L.lane : N - 1;
+        // the next step's actions, in flight during this step
+        const int nrow = arow + 1 == n_act ? 0 : arow + 1;
+        const float4 anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, ma);
+
+        // apply_environment_force + integrate_state (as gsm_step_seg_kernel)
+        KernargParams &pc = late_params();
+        if (L.agent) {
+            const float2 pi = s_pos[m];
+            float Fx = u.x, Fy = u.y;
+            uint64_t cm = cand_prev;
+            while (cm) {
+                const int c = __builtin_ctzll(cm);
+                cm &= cm - 1;
+                const bool ag = c < N;
+                const float2 pj = s_pos[row_entity(c, N)];
+                const float dx = pi.x - pj.x, dy = pi.y - pj.y;
+                const float d2 = dx * dx + dy * dy;
+                const float f = contact_scale(pc, d2, ag ? pc.dmin_aa : pc.dmin_ao);
+                Fx += f * dx;
+                Fy += f * dy;
+            }
+            if (pc.strict && strict_bad(m, pi, N, M, [&](int c) { return s_pos[row_entity(c, N)]; })) {
+                Fx = __builtin_nanf("");
+                Fy = __builtin_nanf("");
+            }
+            const float dt = pc.dt, max_speed = pc.max_speed;
+            v.x = v.x * pc.omd;
+            v.y = v.y * pc.omd;
+            v.x = v.x + (Fx * pc.inv_mass) * dt;
+            v.y = v.y + (Fy * pc.inv_mass) * dt;
+            if (max_speed > 0.0f) {
+                const float sp = sqrtf(v.x * v.x + v.y * v.y);
+                if (sp > max_speed) {
+                    v.x = v.x / sp * max_speed;
+                    v.y = v.y / sp * max_speed;
+                }
+            }
+            float2 np;
+            np.x = pi.x + v.x * dt;
+            np.y = pi.y + v.y * dt;
+            s_pos[m] = np;
+        }
+        wave_sync();
+        t += 1;
+        const bool done = L.live && t >= pc.EL;
+
+        // observation pass on the post-physics positions
+        float2 pm = s_pos[row_entity(m, N)];
+        uint64_t row, cand;
+        int ccnt;
+        bool coinc;
+        obs_sweep<kN, kNo, 1>(p, s, L, s_pos, s_nf, pm, false, oo, row, cand, ccnt, coinc);
+
+        // reward / cost
+        float r = 0.0f;
+        if (L.agent) {
+            const float2 g = s_pos[N + m];
+            const float dx = pm.x - g.x, dy = pm.y - g.y;
+            r = -__builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+        }
+        float rsum = wave_total(r);
+        const int ci = L.agent ? ccnt : 0;
+        const int csum = wave_total(ci);
+        if (L.agent) {
+            KernargParams &q = late_params();
+            (q.reward + eb * N)[um] = p.shared_reward ? rsum : r;
+            (q.cost + eb * N)[um] = (float)ci;
+        }
+        if (p.shared_reward) rsum *= (float)N;
+        if (L.live) {
+            acc.x += rsum;
+            acc.y += (float)csum;
+        }
+        bool reset = false;
+        if (done && p.auto_reset) {
+            reset = true;
+            if (m == 0) late_params().ep_last[L.b] = acc;
+        }
+        if (__any(reset)) {
+            // auto-reset: scenario.reset_world, then the graph part again
+            if (reset) {
+                ep = ep + 1;
+                t = 0;
+                acc = make_float2(0.0f, 0.0f);
+                v = make_float2(0.0f, 0.0f);
+                const uint32_t gid = (uint32_t)(p.env_base + L.b);
+                for (int e = m; e < E; e += M) s_pos[e] = layout_pos(p, gid, (uint32_t)ep, (uint32_t)e);
+            }
+            wave_sync();
+            const float2 pm2 = s_pos[row_entity(m, N)];
+            uint64_t row2, cand2;
+            int cc2;
+            bool coinc2;
+            obs_sweep<kN, kNo, 1>(p, s, L, s_pos, s_nf, pm2, true, 0ull, row2, cand2, cc2, coinc2);
+            if (reset) {
+                pm = pm2;
+                row = row2;
+                cand = cand2;
+                coinc = coinc2;
+            }
+        }
+        const bool relaid = reset;
+        if (!L.live) row = 0;
+
+        // outputs and state of step t
+        KernargParams &q = late_params();
+        float2 *const pos_b = q.pos + eb * E;
+        float2 *const vel_b = q.vel + eb * N;
+        const bool any_statics = p.nf_full || __any(relaid);
+        if (L.live) {
+            float *nf = q.node_feat + eb * E * 7;
+            if (L.agent) {
+                const float2 g = s_pos[N + m];
+                store_row(nf + m * 7, v, pm, make_float2(g.x - pm.x, g.y - pm.y), 0.0f);
+                if (any_statics)
+                    store_row(nf + (N + m) * 7, make_float2(0.0f, 0.0f), g, make_float2(0.0f, 0.0f), 1.0f);
+            } else if (any_statics) {
+                store_row(nf + (N + m) * 7, make_float2(0.0f, 0.0f), pm, make_float2(0.0f, 0.0f), 2.0f);
+            }
+            if (relaid) {
+                for (int e = m; e < E; e += M) pos_b[(uint32_t)e] = s_pos[e];
+            } else if (L.agent) {
+                pos_b[um] = pm;
+            }
+            if (L.agent) vel_b[um] = v;
+            if (L.agent) (q.contact_mask + eb * N)[um] = cand;
+            (q.row_mask + eb * M)[um] = row;
+        }
+        uint8_t deg = 0;
+        if (q.degenerate) {
+            const uint64_t nb = __ballot(L.agent && nonfinite2(pm));
+            deg = (uint8_t)((coinc ? kDegCoincident : 0) | (nb ? kDegNonfinite : 0));
+        }
+        const int edges = __popcll(row) + ((L.live && m == 0) ? 2 * N : 0);
+        const int wave_edges = wave_total(edges);
+        if (wave_live && L.lane == 0) {
+            q.step_count[L.b] = t;
+            q.episode[L.b] = ep;
+            q.ep_acc[L.b] = acc;
+            q.done[L.b] = done ? 1 : 0;
+            q.edge_count[L.b] = wave_edges;
+            if (q.degenerate) q.degenerate[L.b] = deg;
+        }
+
+        // publish the workgroup's edge sum of step t
+        const int par = k & 1;
+        if (L.lane == 0) s_bc[par * kWavesPerBlock + wave] = wave_edges;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int sum = 0;
+            for (int w = 0; w < kWavesPerBlock; ++w) sum += s_bc[par * kWavesPerBlock + w];
+            __hip_atomic_store((gu64 *)(q.roll.gran + (int64_t)k * gridDim.x + blockIdx.x),
+                               ((uint64_t)(k + 1) << 32) | (uint32_t)sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (k == K - 1) q.block_edge_sum[blockIdx.x] = sum;   // read by the emit launch that follows
+        }
+        // the edges of step t - 1 (kept positions and row masks; the counts of
+        // this workgroup's envs are read before block_emit's barrier)
+#ifndef ROLLX_NOEMIT
+        if (k > 0) {
+            BlockPrefix pre;
+            pre.cnt_k = L.lane < kWavesPerBlock ? s_bc[(1 - par) * kWavesPerBlock + L.lane] : 0;
+            KernargParams &qe = late_params();
+#ifdef ROLLX_NOPRE
+            pre.acc = 0;
+#else
+            pre.acc = roll_prefix_part(qe.roll.gran + (int64_t)(k - 1) * gridDim.x, (uint32_t)k, qe.roll.status);
+#endif
+            KernargParams &qs = late_params();
+            block_emit<kN, kNo, 1>(p, s, L, s_prev, oo, pre, s_red, qs.lag.edge_ptr,
+                                   EdgeSink{qs.lag.edge_index, qs.lag.edge_attr, qs.lag.cap}, (uint32_t *)s_nf,
+                                   scr_cap);
+            wave_sync();
+        }
+#endif
+        // keep step t for the next iteration's emission and sweep
+        oo = row;
+        cand_prev = L.agent ? cand : 0ull;
+        if (wave_live) {
+            if (L.lane < E) s_prev[L.lane] = s_pos[L.lane];
+            if (L.lane + kWave < E) s_prev[L.lane + kWave] = s_pos[L.lane + kWave];
+        }
+        u = roll_force<kFmt>(late_params(), anext, L.agent);
+        arow = nrow;
+        wave_sync();
+    }
+}
+
 // Specialisations with compile-time shapes (segment arithmetic folded, G = 1
 // collectives for 24 agents) and action formats; anything else runs the
 // runtime-shape instantiation.
 #define GSM_SEG_SHAPES(X) X(3, 3) X(24, 24)
+#define GSM_ROLL_SHAPES(X) X(24, 24)   // one env per wave
 
 template <bool LAG>
 static const void *pick_step_seg(const DevParams &p) {
@@ -1120,6 +1458,24 @@ static const void *pick_step_seg(const DevParams &p) {
 }
 const void *step_seg_kernel_fn(const DevParams &p) { return pick_step_seg<false>(p); }
 const void *lag_step_seg_kernel_fn(const DevParams &p) { return pick_step_seg<true>(p); }
+
+const void *roll_seg_kernel_fn(const DevParams &p) {
+    if (p.path != kPathSeg) return nullptr;
+#define GSM_PICK(n, no)                                                                  \
+    if (p.N == n && p.No == no && p.G == 1) {                                            \
+        switch (p.action_fmt) {                                                          \
+            case 0: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 0>); \
+            case 1: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 1>); \
+            default: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 2>); \
+        }                                                                                \
+    }
+    GSM_ROLL_SHAPES(GSM_PICK)
+#undef GSM_PICK
+    return nullptr;
+}
+size_t roll_kernel_lds(const DevParams &p) {
+    return (size_t)kWavesPerBlock * (p.wave_lds_step + 8 * p.E) + 64;
+}
 
 const void *emit_seg_kernel_fn(const DevParams &p) {
 #define GSM_PICK(n, no) \

@@ -11,13 +11,13 @@ import os
 from pathlib import Path
 
 LIB_PATH = Path(os.environ.get("GSM_LIB_PATH") or Path(__file__).resolve().parent / "lib" / "libgsm.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 DEGENERATE_COINCIDENT, DEGENERATE_NONFINITE = 1, 2
 
 GSM_OK, GSM_EINVAL, GSM_EHIP, GSM_ESTATE = 0, -1, -2, -3
 GRAPH_SLOTS = 4
 GRAPH_STEP, GRAPH_EMIT, GRAPH_TIME_EACH, GRAPH_TIME_ENDS = 1, 2, 4, 8
-GRAPH_UNFUSED, GRAPH_LAG_ONLY = 16, 32
+GRAPH_UNFUSED, GRAPH_LAG_ONLY, GRAPH_ROLL = 16, 32, 64
 RENDER_EDGES = 1
 ACT_ONEHOT, ACT_INDEX, ACT_CONT = 0, 1, 2
 
@@ -81,6 +81,7 @@ SIGNATURES = {
                                          C.POINTER(GsmOutputs)]),
     "gsm_graph_capture": (C.c_int, [_P, C.c_int32, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int, C.c_int]),
     "gsm_graph_launch": (C.c_int, [_P, C.c_int32, _P]),
+    "gsm_graph_roll_status": (C.c_int, [_P, C.POINTER(C.c_int32)]),
     "gsm_graph_kernel_ms": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                       C.POINTER(C.c_float)]),
     "gsm_attn_aggregate": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_float,

@@ -259,13 +259,16 @@ class GpuBatchEnv:
         ``actions_seq[j % len(actions_seq)]`` (a [T, B, N(,k)] device tensor).
         kernels: "both" (segmented configs: lagged emission, one launch per
         step), "unfused" (step + emit kernel per step), "step", "emit"
-        (re-emits the current edges) or "lag" (lagged step kernels only; the
-        last step's edges are left unemitted — a timing tool).
+        (re-emits the current edges), "lag" (lagged step kernels only; the
+        last step's edges are left unemitted — a timing tool) or "roll"
+        (steps 1..n_steps-1 in one fused rollout launch; one-env-per-wave
+        segmented configs only — GsmError otherwise; with time_ends the
+        events bracket that launch).
         timing: event nodes around every kernel (implies "unfused");
         time_ends: only around the whole graph (per-kernel means over
         back-to-back launches)."""
         flags = {"both": 0, "unfused": _lib.GRAPH_UNFUSED, "step": _lib.GRAPH_STEP, "emit": _lib.GRAPH_EMIT,
-                 "lag": _lib.GRAPH_LAG_ONLY}[kernels]
+                 "lag": _lib.GRAPH_LAG_ONLY, "roll": _lib.GRAPH_ROLL}[kernels]
         if timing:
             flags |= _lib.GRAPH_TIME_EACH
         if time_ends:
@@ -295,6 +298,13 @@ class GpuBatchEnv:
     @_ranged("gsm.replay")
     def replay(self, slot: int = 0) -> None:
         self._chk(self.lib.gsm_graph_launch(self._h, int(slot), self._stream()), "gsm_graph_launch")
+
+    def roll_gave_up(self) -> bool:
+        """Whether a bounded wait of a fused rollout launch timed out since
+        the last call (outputs of that launch invalid); clears the flag."""
+        v = C.c_int32()
+        self._chk(self.lib.gsm_graph_roll_status(self._h, C.byref(v)), "gsm_graph_roll_status")
+        return bool(v.value)
 
     def graph_kernel_ms(self, slot: int = 0):
         """(mean step-kernel ms, mean emit-kernel ms, whole-graph ms) of the

@@ -35,7 +35,8 @@ extern "C" {
 /* 4: lagged-emission graph chains (GSM_GRAPH_UNFUSED / _LAG_ONLY), gsm_render
  * 5: degenerate-state handling: gsm_config.strict_degenerate,
  *    gsm_buffers.degenerate */
-#define GSM_ABI_VERSION 5
+/* 6: fused rollout graphs (GSM_GRAPH_ROLL, gsm_graph_roll_status) */
+#define GSM_ABI_VERSION 6
 
 typedef enum gsm_status {
     GSM_OK = 0,
@@ -239,6 +240,15 @@ int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream);
 #define GSM_GRAPH_TIME_ENDS 8
 #define GSM_GRAPH_UNFUSED 16
 #define GSM_GRAPH_LAG_ONLY 32
+/* GSM_GRAPH_ROLL: steps 1 .. n_steps-1 run in ONE launch (segmented configs
+ * with one env per wave, e.g. 24 agents + 24 obstacles; the whole batch in one
+ * residency round). Each wave keeps its env's state on chip across the steps;
+ * workgroups hand the CSR edge-count prefix to each other through tagged
+ * granules (bounded waits). Outputs after the graph are identical to the
+ * lagged chain's. Combines with GSM_GRAPH_TIME_ENDS only (the events then
+ * bracket the rollout launch: gsm_graph_kernel_ms gives its time per step);
+ * GSM_EINVAL where the config has no rollout kernel. */
+#define GSM_GRAPH_ROLL 64
 int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t action_stride_bytes,
                       int32_t n_actions, int32_t n_steps, int action_fmt, int flags);
 /* As gsm_graph_capture (both kernels, no timing events), with the j-th
@@ -246,6 +256,10 @@ int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t 
 int gsm_graph_capture_into(gsm_handle *h, int32_t slot, const void *actions, int64_t action_stride_bytes,
                            int32_t n_actions, int32_t n_steps, int action_fmt, const gsm_outputs *per_step);
 int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream);
+/* After GSM_GRAPH_ROLL launches have completed: *gave_up = 1 if any bounded
+ * wait of a rollout launch timed out since the last call (its outputs are
+ * then invalid), else 0. Clears the flag. */
+int gsm_graph_roll_status(gsm_handle *h, int32_t *gave_up);
 /* After a timed launch of `slot` has completed: mean duration (ms) of the
  * step and emit kernels (TIME_EACH), and the whole graph (both flags). */
 int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_mean_ms, float *emit_mean_ms,
