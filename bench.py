@@ -7,9 +7,13 @@ owns 8192 envs with global Philox env ids, BASELINE configs[4] at N=8).
 
 A "step" = one env.step of every env on the GPU: action force, pairwise
 contact physics, integration, reward, collision cost, done/auto-reset, node
-features and the packed COO edge list (inside a graph the
-segmented configs run one launch per step — step j+1's kernel first emits
-step j's edges — plus one emit launch at the end of the graph). Actions
+features and the packed COO edge list, every output of every step written to
+HBM. Inside a graph the one-env-per-wave segmented configs (the
+headline) run all steps of the episode graph in ONE fused rollout launch
+(GSM_GRAPH_ROLL: env state kept on chip, the CSR prefix handed between
+workgroups in-launch); the other segmented configs one launch per step (step
+j+1's kernel first emits step j's edges); `--no-roll` / `--unfused` select
+those chains instead. Actions
 are pre-generated on device (100 x B x N int32, uniform over the 5 discrete
 actions) so the timed region has no host work; the K timed steps are
 replayed from HIP graphs of one episode (100 steps) each, with the per-episode
@@ -90,6 +94,18 @@ def lag_extra_bytes(B, N, No, total_edges, seg=True):
         W, ka = (M + 63) // 64, (N + 63) // 64
         masks = 8 * (M * W - No * (W - ka))
     return B * (masks + 4 + 8) + 12 * total_edges
+
+
+def roll_step_bytes(B, N, No, EL, action_bytes, total_edges):
+    """Algorithmic HBM bytes per step of the fused rollout launch: the state
+    stays on chip, so a step reads only its actions; it writes everything a
+    step kernel writes (step_kernel_bytes) plus the emission of the previous
+    step (edge_ptr entry, 12 B per edge). The launch's one-time state load is
+    left out (under 1% over 100 steps)."""
+    E, M = 2 * N + No, N + No
+    writes = 8 * N + 8 * N + 28 * N + 4 * N + 4 * N + 8 * N + 8 * M + 16 + 1 + 4 + 8
+    reset = (8 * (E - N) + 28 * (E - N) + 8) / EL
+    return B * (action_bytes * N + writes + reset) + 12 * total_edges
 
 
 def ragged_kernel_bytes(env, EL, action_bytes, total_edges):
@@ -282,6 +298,8 @@ def parse_args(argv=None):
     ap.add_argument("--eager", action="store_true", help="launch steps eagerly instead of HIP graphs")
     ap.add_argument("--unfused", action="store_true",
                     help="two launches per step in the graphs (no lagged emission)")
+    ap.add_argument("--no-roll", action="store_true",
+                    help="one launch per step (lagged chain) even where a fused rollout launch exists")
     # launcher self-test only (tests/test_bench_launcher.py): a CPU stand-in env
     # module and gloo; the line it prints is marked as not a measurement
     ap.add_argument("--selftest-env", default=None, help=argparse.SUPPRESS)
@@ -312,7 +330,9 @@ def _spawned_rank(argv, rank, world, port):
     in it yet)."""
     os.environ.update(RANK=str(rank), LOCAL_RANK=str(rank), WORLD_SIZE=str(world),
                       LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    run_rank(parse_args(argv))
+    rc = run_rank(parse_args(argv))
+    if rc:
+        sys.exit(rc)
 
 
 def launch_ranks(args, argv):
@@ -415,14 +435,29 @@ def run_rank(args):
     chunk = min(K, EL)
     n_chunks, rem = divmod(K, chunk)
     gk = "unfused" if args.unfused else "both"
+    roll = not (args.unfused or args.no_roll or args.eager or stub)
+
+    def capture(n, slot):
+        """A graph of n steps: the fused rollout where the config has one
+        (n >= 2), else the lagged / two-kernel chain."""
+        nonlocal roll
+        if roll and n >= 2:
+            try:
+                env.capture(actions, n, timing=False, slot=slot, kernels="roll")
+                return
+            except Exception as e:   # GsmError: no rollout kernel for this config
+                log(f"no fused rollout for this config ({e}); one launch per step")
+                roll = False
+        env.capture(actions, n, timing=False, slot=slot, kernels=gk)
+
     if not args.eager:
         if W > 0:
-            env.capture(actions, W, timing=False, slot=2, kernels=gk)
+            capture(W, 2)
         if A > 0:   # slot 3 is re-captured later by the roofline timing
-            env.capture(actions, A, timing=False, slot=3, kernels=gk)
-        env.capture(actions, chunk, timing=False, slot=0, kernels=gk)
+            capture(A, 3)
+        capture(chunk, 0)
         if rem:
-            env.capture(actions, rem, timing=False, slot=1, kernels=gk)
+            capture(rem, 1)
 
     def run_steps(n, slot):
         if args.eager:
@@ -472,6 +507,17 @@ def run_rank(args):
     else:
         times = [elapsed]
     elapsed = max(times)
+    # a bounded in-launch wait of a fused rollout that timed out leaves invalid
+    # outputs: no measurement (decided on every rank together)
+    bad = 1.0 if (roll and env.roll_gave_up()) else 0.0
+    if world > 1:
+        bad = float(all_reduce_metrics(torch.tensor([bad, 0.0, 0.0], dtype=torch.float64, device=dev))[0].item())
+    if bad:
+        log("ERROR: a fused rollout launch gave up waiting on a predecessor; no valid measurement")
+        env.close()
+        if world > 1:
+            dist.destroy_process_group()
+        return 3
     # final episode metrics over all ranks (the same RCCL all-reduce)
     metrics.copy_(env.episode_metrics())
     all_reduce_metrics(metrics)
@@ -493,7 +539,7 @@ def run_rank(args):
     # add their own packet time to every launch.
     roofline = None
     if not args.no_kernel_timing and not args.eager and not stub:
-        roofline = kernel_roofline(env, cfg, actions, args, N, B, EL)
+        roofline = kernel_roofline(env, cfg, actions, args, N, B, EL, roll)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not stub:
@@ -516,7 +562,8 @@ def run_rank(args):
                        "episode_length": EL, "mean_edges_per_env": round(total_edges / B, 2),
                        "parallelism": f"env-sharded x{world} (no data-path collective)",
                        "launch": "eager" if args.eager else ("hip-graph per 100-step episode" + (
-                           ", lagged emission (one launch per step)" if (seg_cfg and not args.unfused)
+                           ": all 100 steps in one fused rollout launch (state on chip, in-launch CSR prefix)"
+                           if roll else ", lagged emission (one launch per step)" if (seg_cfg and not args.unfused)
                            else ", step + emit launch per step"))},
             "timed_region": {"untimed_steps_before": P, "align_steps": A,
                              "episode_boundaries": boundaries_in(P, K, EL),
@@ -536,12 +583,13 @@ def run_rank(args):
     return 0
 
 
-def kernel_roofline(env, cfg, actions, args, N, B, EL):
+def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False):
     import torch
     L = args.kernel_launches
     seg = (N + cfg.n_obstacles) <= 64 and not cfg.ragged
-    lag = seg and not args.unfused   # segmented chains: lagged emission
-    env.capture(actions, L, slot=3, kernels="lag" if lag else "step", time_ends=True)
+    lag = seg and not args.unfused and not roll   # segmented chains: lagged emission
+    # the fused rollout: events around its launch of L steps (time per step)
+    env.capture(actions, L, slot=3, kernels="roll" if roll else "lag" if lag else "step", time_ends=True)
     env.replay(3)
     torch.cuda.synchronize()
     step_ms = env.graph_kernel_ms(3)[0]
@@ -553,6 +601,10 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL):
     if cfg.ragged:
         sb, eb = ragged_kernel_bytes(env, EL, 4, edges_now)
         names = ("gsm_step_ragged_kernel", "gsm_emit_ragged_kernel")
+    elif roll:
+        sb = roll_step_bytes(B, N, cfg.n_obstacles, EL, 4, edges_now)
+        eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)
+        names = (f"gsm_roll_seg_kernel (per step of a {L}-step launch)", "gsm_emit_seg_kernel")
     else:
         sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4, seg, env.sizes.envs_per_block)
         if lag:
@@ -562,12 +614,12 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL):
         names = (f"gsm_step_{fam}_kernel" + ("<lagged emission>" if lag else ""), f"gsm_emit_{fam}_kernel")
     kern = {"step": dict(kernel=names[0], ms=step_ms, bytes=sb, gbs=sb / (step_ms * 1e-3) / 1e9),
             "emit": dict(kernel=names[1], ms=emit_ms, bytes=eb, gbs=eb / (emit_ms * 1e-3) / 1e9)}
-    # a lagged chain runs the emit kernel once per graph, the step kernel every step
-    dom = "step" if (lag or step_ms >= emit_ms) else "emit"
+    # a lagged chain / rollout runs the emit kernel once per graph, the step kernel every step
+    dom = "step" if (lag or roll or step_ms >= emit_ms) else "emit"
     k = kern[dom]
     other = kern["emit" if dom == "step" else "step"]
     hbm_frac = k["gbs"] / HBM_PEAK_GBS
-    pkey = f"{'lag' if (lag and dom == 'step') else dom}:{cfg.scenario}:N{N}:B{B}"
+    pkey = f"{'roll' if (roll and dom == 'step') else 'lag' if (lag and dom == 'step') else dom}:{cfg.scenario}:N{N}:B{B}"
     pmc, note = pmc_entry(pkey)
     valu = None
     if pmc and pmc.get("valu_insts_per_launch"):
@@ -592,7 +644,8 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL):
                     pmc=dict(key=pkey, status=note, valu=valu,
                              source=pmc.get("source") if pmc else None),
                     algorithmic_bytes_per_launch=int(k["bytes"]), mean_launch_us=round(k["ms"] * 1e3, 3),
-                    timing=f"HIP events around {L} back-to-back graph launches of the kernel",
+                    timing=(f"HIP events around one fused rollout launch of {L} steps (time per step)" if roll
+                            else f"HIP events around {L} back-to-back graph launches of the kernel"),
                     other_kernel=dict(kernel=other["kernel"], achieved=round(other["gbs"], 1),
                                       algorithmic_bytes_per_launch=int(other["bytes"]),
                                       mean_launch_us=round(other["ms"] * 1e3, 3)))

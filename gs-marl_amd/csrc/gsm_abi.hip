@@ -496,15 +496,16 @@ int gsm_graph_capture_into(gsm_handle *h, int32_t slot, const void *actions, int
     return capture_impl(h, slot, actions, stride, n_actions, n_steps, action_fmt, 0, per_step);
 }
 
-// Fused rollout graph (GSM_GRAPH_ROLL): step_0, a zeroing memset of the
-// granules, ONE gsm_roll_seg_kernel launch for steps 1 .. T-1 (it emits steps
-// 0 .. T-2), emit_{T-1}. Every output equals the lagged chain's.
+// Fused rollout graph (GSM_GRAPH_ROLL): a zeroing memset of the granules, ONE
+// gsm_roll_seg_kernel launch for all n_steps steps (it emits the edges of all
+// but the last), the emit launch for the last step. Every output equals the
+// lagged chain's.
 static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_t stride, int32_t n_actions,
                         int32_t n_steps, int action_fmt, int flags) {
     if (flags & ~(GSM_GRAPH_ROLL | GSM_GRAPH_TIME_ENDS))
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL combines with GSM_GRAPH_TIME_ENDS only");
     if (!actions || n_actions < 1 || stride < 0) return fail(h, GSM_EINVAL, "bad capture arguments");
-    if (n_steps < 2) return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL needs n_steps >= 2");
+    if (n_steps < 1) return fail(h, GSM_EINVAL, "n_steps must be >= 1");
     if (action_fmt < GSM_ACT_ONEHOT || action_fmt > GSM_ACT_CONT) return fail(h, GSM_EINVAL, "bad action_fmt");
     gsm::DevParams p = h->dp;
     p.mode = GSM_MODE_STEP;
@@ -528,10 +529,6 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: the batch exceeds one residency round of the rollout kernel");
     gsm_handle::Slot &sl = h->slots[slot];
     drop_slot(sl);
-    if (!h->bsum_alt) {
-        e = hipMalloc(&h->bsum_alt, (size_t)h->sz.n_blocks * sizeof(int32_t) + 16);
-        if (e != hipSuccess) { h->bsum_alt = nullptr; return hip_fail(h, e, "hipMalloc (edge-sum buffer)"); }
-    }
     if (!h->roll_status) {
         e = hipMalloc(&h->roll_status, 16);
         if (e == hipSuccess) e = hipMemset(h->roll_status, 0, 16);
@@ -541,8 +538,9 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         e = hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking);
         if (e != hipSuccess) return hip_fail(h, e, "hipStreamCreate");
     }
-    const int K = n_steps - 1;
-    const size_t gran_bytes = (size_t)K * nb * sizeof(uint64_t);   // a multiple of 16 (nb even) or padded
+    const int K = n_steps;
+    // aggregates [K][nb], then inclusive prefixes [K][nb] (look-back)
+    const size_t gran_bytes = 2 * (size_t)K * nb * sizeof(uint64_t);
     const size_t gran_alloc = (gran_bytes + 15) & ~(size_t)15;
     e = hipMalloc(&sl.gran, gran_alloc);
     if (e != hipSuccess) { sl.gran = nullptr; return hip_fail(h, e, "hipMalloc (rollout granules)"); }
@@ -555,35 +553,8 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     e = hipGraphCreate(&sl.graph, 0);
     if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipGraphCreate"); }
     hipGraphNode_t prev = nullptr;
-    auto add_kernel = [&](const void *fn, const gsm::DevParams &kp_params, int grid, size_t lds) -> hipError_t {
-        hipKernelNodeParams kp = {};
-        gsm::DevParams q = kp_params;
-        void *args[] = {&q};
-        kp.func = const_cast<void *>(fn);
-        kp.gridDim = dim3(grid);
-        kp.blockDim = dim3(gsm::block_threads(q));
-        kp.sharedMemBytes = (unsigned)lds;
-        kp.kernelParams = args;
-        kp.extra = nullptr;
-        hipGraphNode_t n;
-        const hipError_t r = hipGraphAddKernelNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0, &kp);
-        if (r == hipSuccess) prev = n;
-        return r;
-    };
-    auto add_event = [&](hipEvent_t ev) -> hipError_t {
-        hipGraphNode_t n;
-        const hipError_t r = hipGraphAddEventRecordNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0, ev);
-        if (r == hipSuccess) prev = n;
-        return r;
-    };
-    const char *what = "step kernel node";
-    // step 0: the plain step kernel, writing its edge sums to the second half
-    gsm::DevParams p0 = p;
-    p0.actions = actions;
-    p0.block_edge_sum = h->bsum_alt;
-    e = add_kernel(gsm::step_kernel_fn(p0), p0, nb, gsm::step_kernel_lds(p0));
-    if (e == hipSuccess) {
-        what = "memset node";
+    const char *what = "memset node";
+    {
         hipMemsetParams mp = {};
         mp.dst = sl.gran;
         mp.elementSize = 4;
@@ -591,23 +562,49 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         mp.height = 1;
         mp.pitch = gran_alloc;
         mp.value = 0;
+        e = hipGraphAddMemsetNode(&prev, sl.graph, nullptr, 0, &mp);
+    }
+    auto add_event = [&](hipEvent_t ev) -> hipError_t {
         hipGraphNode_t n;
-        e = hipGraphAddMemsetNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0, &mp);
+        const hipError_t r = hipGraphAddEventRecordNode(&n, sl.graph, &prev, 1, ev);
+        if (r == hipSuccess) prev = n;
+        return r;
+    };
+    if (e == hipSuccess && ends) { what = "event node"; e = add_event(sl.events[0]); }
+    // all steps in one launch; the last step's sums go to the bound edge-sum
+    // buffer (later eager emits read it); edges go to the bound outputs
+    p.actions = actions;
+    p.lag = gsm::DevParams::Lag{p.block_edge_sum, p.edge_count, p.edge_ptr, p.edge_index, p.edge_attr,
+                                p.edge_capacity};
+    p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, 0, sl.gran, h->roll_status};
+    if (e == hipSuccess) {
+        what = "rollout kernel node";
+        hipKernelNodeParams kp = {};
+        void *args[] = {&p};
+        kp.func = const_cast<void *>(roll_fn);
+        kp.gridDim = dim3(nb);
+        kp.blockDim = dim3(gsm::block_threads(p));
+        kp.sharedMemBytes = (unsigned)roll_lds;
+        kp.kernelParams = args;
+        kp.extra = nullptr;
+        hipGraphNode_t n;
+        e = hipGraphAddKernelNode(&n, sl.graph, &prev, 1, &kp);
         if (e == hipSuccess) prev = n;
     }
-    if (e == hipSuccess && ends) { what = "event node"; e = add_event(sl.events[0]); }
-    // steps 1 .. T-1 in one launch; its final sums go to the bound half
-    gsm::DevParams pr = p;
-    pr.actions = (const char *)actions + (int64_t)(1 % n_actions) * stride;
-    pr.block_edge_sum = h->dp.block_edge_sum;
-    pr.lag = gsm::DevParams::Lag{h->bsum_alt, p.edge_count, p.edge_ptr, p.edge_index, p.edge_attr,
-                                 p.edge_capacity};
-    pr.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 1, K, 0, sl.gran, h->roll_status};
-    if (e == hipSuccess) { what = "rollout kernel node"; e = add_kernel(roll_fn, pr, nb, roll_lds); }
     if (e == hipSuccess && ends) { what = "event node"; e = add_event(sl.events[1]); }
-    if (e == hipSuccess) {
+    if (e == hipSuccess) {   // the last step's edges (see gsm_roll_seg_kernel)
         what = "emit kernel node";
-        e = add_kernel(gsm::emit_kernel_fn(pr), pr, gsm::grid_blocks(pr), gsm::emit_kernel_lds(pr));
+        hipKernelNodeParams kp = {};
+        void *args[] = {&p};
+        kp.func = const_cast<void *>(gsm::emit_kernel_fn(p));
+        kp.gridDim = dim3(gsm::grid_blocks(p));
+        kp.blockDim = dim3(gsm::block_threads(p));
+        kp.sharedMemBytes = (unsigned)gsm::emit_kernel_lds(p);
+        kp.kernelParams = args;
+        kp.extra = nullptr;
+        hipGraphNode_t n;
+        e = hipGraphAddKernelNode(&n, sl.graph, &prev, 1, &kp);
+        if (e == hipSuccess) prev = n;
     }
     if (e != hipSuccess) {
         drop_slot(sl);
@@ -620,11 +617,11 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     e = hipGraphUpload(sl.exec, h->cap_stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->cap_stream);
     if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipGraphUpload"); }
-    // timing (TIME_ENDS): the events bracket the rollout kernel alone, so
+    // timing (TIME_ENDS): the events bracket the rollout launch alone, so
     // gsm_graph_kernel_ms reports its time per step
     sl.each = false;
     sl.kern = GSM_GRAPH_STEP;
-    sl.steps = ends ? K : n_steps;
+    sl.steps = n_steps;
     return GSM_OK;
 }
 

@@ -1119,9 +1119,12 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
 // wait is normally already satisfied. A workgroup waits only on workgroups
 // with smaller index (dispatched before it), so the chain always progresses;
 // every wait is bounded (kRollSpinTicks, then p.roll.status is set and the
-// launch drains). Step t_first - 1's edges are emitted first (prefix from the
-// previous launch's sums, as the lagged kernel); the last step's edges are
-// left to the emit launch that ends the graph.
+// launch drains). The state the launch starts from had its edges emitted by
+// whatever ran before. The last step's edges are left to an emit launch: in
+// the shared output buffers they must land after every workgroup's emission of
+// the earlier steps (a workgroup may trail its successors by several steps),
+// which a kernel boundary orders for ~1.5 us where a grid barrier over 2048
+// workgroups would cost ~10 us (MI355X_MICROARCH.md price list).
 #ifndef GSM_ROLL_ATTR   // all 8 waves per SIMD resident (2048 workgroups at 8192 envs: one residency round)
 #define GSM_ROLL_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
 #endif
@@ -1144,27 +1147,30 @@ __device__ __forceinline__ uint64_t roll_wait(const uint64_t *g, uint32_t tag, u
     }
 }
 
-// this thread's part of the sum of the granules of workgroups [0, blockIdx.x)
-// (loads at clamped addresses first, tags checked afterwards)
-__device__ __forceinline__ int roll_prefix_part(const uint64_t *gran_k, uint32_t tag, uint32_t *status) {
-    const int w = (int)blockIdx.x, tid = (int)threadIdx.x;
+// Decoupled look-back over the preceding workgroups (ONE wave; wave-uniform
+// result): windows of 64 predecessors, nearest first; the nearest one whose
+// inclusive prefix is published ends the walk (its inclusive + the aggregates
+// of those in between), otherwise the window's aggregates are added and the
+// walk moves on. Aggregates were published an iteration earlier, so the walk
+// never waits on an inclusive prefix; an aggregate read early is re-polled.
+__device__ __forceinline__ int roll_lookback(const uint64_t *agg_k, const uint64_t *inc_k, uint32_t tag,
+                                             uint32_t *status, int lane) {
     int acc = 0;
-    for (int base = 0; base < w; base += 8 * kBlock) {
-        uint64_t x[8];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int i = base + tid + j * kBlock;
-            x[j] = __hip_atomic_load((const gu64 *)(gran_k + (i < w ? i : w - 1)), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
-        }
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const int i = base + tid + j * kBlock;
-            if (i < w) {
-                if ((uint32_t)(x[j] >> 32) != tag) x[j] = roll_wait(gran_k + i, tag, status);
-                acc += (int)(uint32_t)x[j];
-            }
-        }
+    for (int hi = (int)blockIdx.x; hi > 0; hi -= kWave) {
+        const int idx = hi - 1 - lane;                      // lane 0 = nearest predecessor
+        const int ci = idx >= 0 ? idx : 0;
+        const uint64_t xi = __hip_atomic_load((const gu64 *)(inc_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t xa = __hip_atomic_load((const gu64 *)(agg_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool valid = idx >= 0;
+        const uint64_t have = __ballot(valid && (uint32_t)(xi >> 32) == tag);
+        const int j = have ? __builtin_ctzll(have) : kWave;   // wave-uniform
+        // aggregates of lanes < j (all valid lanes when no inclusive was found)
+        const bool need = valid && lane < j;
+        if (need && (uint32_t)(xa >> 32) != tag) xa = roll_wait(agg_k + ci, tag, status);
+        int v = need ? (int)(uint32_t)xa : 0;
+        if (lane == j) v = (int)(uint32_t)xi;
+        acc += wave_total(v);
+        if (have) break;
     }
     return acc;
 }
@@ -1220,10 +1226,9 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     const bool wave_live = L0.b < p.B;
     const int64_t eb = wave_live ? L0.b : 0;
     
-    // ---- step t_first - 1's state and step t_first's actions (p.actions), the
-    // previous launch's edge sums; its edges first, as the lagged kernel
+    // ---- the state before step t_first and step t_first's actions
+    // (p.actions); the edges of that state were emitted by whatever ran before
     SegIn in = seg_load<kN, kNo, kFmt, true>(p, s, L0);
-    const BlockPrefix pre0 = block_prefix_loads(p.lag.block_sum, p.lag.edge_count, p.B, 1, p.pos);
     seg_load_finish<kN, kNo, kFmt, true>(p, L0, in);
     int t = in.t, ep = in.ep;
     float2 acc = in.acc, v = in.v, u = in.u;
@@ -1231,12 +1236,6 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     if (wave_live) {
         if (L0.lane < E) s_pos[L0.lane] = in.x0;
         if (L0.lane + kWave < E) s_pos[L0.lane + kWave] = in.x1;
-    }
-    wave_sync();
-    {
-        KernargParams &q = late_params();
-        block_emit<kN, kNo, 1>(p, s, L0, s_pos, oo, pre0, s_red, q.lag.edge_ptr,
-                               EdgeSink{q.lag.edge_index, q.lag.edge_attr, q.lag.cap}, (uint32_t *)s_nf, scr_cap);
     }
     wave_sync();
 
@@ -1414,7 +1413,22 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
 #ifdef ROLLX_NOPRE
             pre.acc = 0;
 #else
-            pre.acc = roll_prefix_part(qe.roll.gran + (int64_t)(k - 1) * gridDim.x, (uint32_t)k, qe.roll.status);
+            // wave 0 walks back over the predecessors and publishes this
+            // workgroup's inclusive prefix of step t - 1 at once
+            pre.acc = 0;
+            if (wave == 0) {
+                const int64_t kb = (int64_t)(k - 1) * gridDim.x;
+                const int ex = roll_lookback(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
+                                             (uint32_t)k, qe.roll.status, L.lane);
+                int own = 0;
+                for (int w = 0; w < kWavesPerBlock; ++w) own += s_bc[(1 - par) * kWavesPerBlock + w];
+                if (L.lane == 0) {
+                    pre.acc = ex;
+                    __hip_atomic_store((gu64 *)(qe.roll.gran + (int64_t)K * gridDim.x + kb + blockIdx.x),
+                                       ((uint64_t)k << 32) | (uint32_t)(ex + own), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
 #endif
             KernargParams &qs = late_params();
             block_emit<kN, kNo, 1>(p, s, L, s_prev, oo, pre, s_red, qs.lag.edge_ptr,

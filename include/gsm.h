@@ -240,14 +240,15 @@ int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream);
 #define GSM_GRAPH_TIME_ENDS 8
 #define GSM_GRAPH_UNFUSED 16
 #define GSM_GRAPH_LAG_ONLY 32
-/* GSM_GRAPH_ROLL: steps 1 .. n_steps-1 run in ONE launch (segmented configs
- * with one env per wave, e.g. 24 agents + 24 obstacles; the whole batch in one
+/* GSM_GRAPH_ROLL: all n_steps steps run in ONE launch, then the last step's
+ * edge emission in a second (segmented configs with
+ * one env per wave, e.g. 24 agents + 24 obstacles; the whole batch in one
  * residency round). Each wave keeps its env's state on chip across the steps;
  * workgroups hand the CSR edge-count prefix to each other through tagged
  * granules (bounded waits). Outputs after the graph are identical to the
- * lagged chain's. Combines with GSM_GRAPH_TIME_ENDS only (the events then
- * bracket the rollout launch: gsm_graph_kernel_ms gives its time per step);
- * GSM_EINVAL where the config has no rollout kernel. */
+ * lagged chain's (every step's edges are emitted). Combines with GSM_GRAPH_TIME_ENDS only (the events then bracket
+ * the launch: gsm_graph_kernel_ms gives its time per step); GSM_EINVAL where
+ * the config has no rollout kernel. */
 #define GSM_GRAPH_ROLL 64
 int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t action_stride_bytes,
                       int32_t n_actions, int32_t n_steps, int action_fmt, int flags);

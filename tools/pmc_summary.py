@@ -16,7 +16,9 @@ for f in glob.glob(os.path.join(root, "p*", "**", "*counter_collection.csv"), re
             name = row.get("Kernel_Name", "")
             if "gsm" not in name:
                 continue
-            if "step" in name:   # the lagged-emission step kernel: template argument kLag = true
+            if "roll" in name:   # the fused rollout kernel (one launch per graph)
+                short = "roll"
+            elif "step" in name:   # the lagged-emission step kernel: template argument kLag = true
                 short = "lag" if "true>" in name else "step"
             else:
                 short = "emit" if "emit" in name else name[:40]

@@ -8,6 +8,10 @@ records the hash of the kernel sources it was collected on (bench.kernel_src_has
 bench.py ignores it once the sources change, so stale counters never reach a
 bench line.
 
+The fused rollout kernel ("roll") runs ROLL_STEPS steps per launch (env,
+default 100: a 100-step graph); its entry is normalised to one step, so that
+bench.py compares it with the launch time per step.
+
 Usage: python tools/pmc_traffic.py OUT_JSON [KINDS@]KEY_PREFIX=SUMMARY_DIR ...
   e.g. h:navigation:N24:B8192=gpurun_out/pmc_h  (keys: step:navigation:N24:B8192, emit:...)
        lag@h:navigation:N24:B8192=gpurun_out/pmc_h_lag  (only the lagged step kernel)
@@ -52,6 +56,13 @@ for spec in sys.argv[2:]:
                       ("SQ_WAVE_CYCLES", "wave_quad_cycles_per_launch")):
             if cn in c:
                 e[k] = c[cn]
+        if kern == "roll":   # per step of the launch
+            n = int(os.environ.get("ROLL_STEPS", "100"))
+            for k in ("hbm_bytes_per_launch", "read_bytes_corrected", "write_bytes", "valu_insts_per_launch",
+                      "salu_insts_per_launch", "lds_insts_per_launch", "wave_quad_cycles_per_launch"):
+                if k in e:
+                    e[k] = round(e[k] / n, 1)
+            e["per"] = f"step (counters of one {n}-step launch / {n})"
         ent[f"{kern}:{key.split(':', 1)[1]}"] = e
 json.dump(res, open(out_path, "w"), indent=1, sort_keys=True)
 print(json.dumps(res, indent=1))

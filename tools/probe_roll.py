@@ -32,11 +32,17 @@ def main():
     ap.add_argument("--N", type=int, default=24)
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--sweep", action="store_true", help="whole-graph time vs graph length (fixed cost)")
     a = ap.parse_args()
     env = GpuBatchEnv(EnvConfig(n_agents=a.N, n_envs=a.B, seed=1234), "cuda:0")
     acts = torch.randint(0, 5, (100, a.B, a.N), dtype=torch.int32, device="cuda:0")
     env.reset(seed=1234, sync_edges=False)
     out = {"B": a.B, "N": a.N, "T": a.T}
+    if a.sweep:
+        for kern in ("both", "roll"):
+            for T in (1, 2, 5, 20, 100):
+                env.capture(acts, T, slot=0, kernels=kern)
+                out[f"{kern}_T{T}_graph_us"] = round(timed(env, 0, a.reps) * 1e3, 2)
     for kern in ("both", "roll"):
         env.capture(acts, a.T, slot=0, kernels=kern)
         ms = timed(env, 0, a.reps)
