@@ -97,14 +97,16 @@ def lag_extra_bytes(B, N, No, total_edges, seg=True):
 
 
 def roll_step_bytes(B, N, No, EL, action_bytes, total_edges):
-    """Algorithmic HBM bytes per step of the fused rollout launch: the state
-    stays on chip, so a step reads only its actions; it writes everything a
-    step kernel writes (step_kernel_bytes) plus the emission of the previous
-    step (edge_ptr entry, 12 B per edge). The launch's one-time state load is
-    left out (under 1% over 100 steps)."""
-    E, M = 2 * N + No, N + No
-    writes = 8 * N + 8 * N + 28 * N + 4 * N + 4 * N + 8 * N + 8 * M + 16 + 1 + 4 + 8
-    reset = (8 * (E - N) + 28 * (E - N) + 8) / EL
+    """Algorithmic HBM bytes per step of the fused rollout launch. The
+    simulator state (positions, velocities, masks, counters) stays on chip and
+    is loaded / stored once per launch (left out: under 1% over 100 steps); a
+    step reads its actions and writes its observation outputs: the agent
+    node-feature rows, reward, cost, done, and (one iteration later) the
+    edge_ptr entry and 12 B per edge; at an episode end the static node rows
+    and the episode metrics, amortised over the episode."""
+    E = 2 * N + No
+    writes = 28 * N + 4 * N + 4 * N + 1 + 8
+    reset = (28 * (E - N) + 8) / EL
     return B * (action_bytes * N + writes + reset) + 12 * total_edges
 
 

@@ -1241,6 +1241,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
 
     const int K = p.roll.K, n_act = p.roll.n_actions;
     int arow = p.roll.t_first % n_act;                      // action row of the current step
+    uint8_t deg = 0;                                        // App. A S16 flags of the final state
     for (int k = 0; k < K; ++k) {
         // lane-derived values re-formed every iteration (an asm barrier): held
         // across the loop they would pin their hoisted addresses in VGPRs
@@ -1352,10 +1353,11 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         const bool relaid = reset;
         if (!L.live) row = 0;
 
-        // outputs and state of step t
+        // the step's observation outputs (node features, reward / cost above,
+        // done; edges one iteration on); the simulator state (positions,
+        // velocities, masks, counters) stays on chip and is stored once, after
+        // the loop
         KernargParams &q = late_params();
-        float2 *const pos_b = q.pos + eb * E;
-        float2 *const vel_b = q.vel + eb * N;
         const bool any_statics = p.nf_full || __any(relaid);
         if (L.live) {
             float *nf = q.node_feat + eb * E * 7;
@@ -1367,30 +1369,14 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             } else if (any_statics) {
                 store_row(nf + (N + m) * 7, make_float2(0.0f, 0.0f), pm, make_float2(0.0f, 0.0f), 2.0f);
             }
-            if (relaid) {
-                for (int e = m; e < E; e += M) pos_b[(uint32_t)e] = s_pos[e];
-            } else if (L.agent) {
-                pos_b[um] = pm;
-            }
-            if (L.agent) vel_b[um] = v;
-            if (L.agent) (q.contact_mask + eb * N)[um] = cand;
-            (q.row_mask + eb * M)[um] = row;
         }
-        uint8_t deg = 0;
-        if (q.degenerate) {
+        if (k == K - 1 && q.degenerate) {
             const uint64_t nb = __ballot(L.agent && nonfinite2(pm));
             deg = (uint8_t)((coinc ? kDegCoincident : 0) | (nb ? kDegNonfinite : 0));
         }
         const int edges = __popcll(row) + ((L.live && m == 0) ? 2 * N : 0);
         const int wave_edges = wave_total(edges);
-        if (wave_live && L.lane == 0) {
-            q.step_count[L.b] = t;
-            q.episode[L.b] = ep;
-            q.ep_acc[L.b] = acc;
-            q.done[L.b] = done ? 1 : 0;
-            q.edge_count[L.b] = wave_edges;
-            if (q.degenerate) q.degenerate[L.b] = deg;
-        }
+        if (wave_live && L.lane == 0) q.done[L.b] = done ? 1 : 0;
 
         // publish the workgroup's edge sum of step t
         const int par = k & 1;
@@ -1447,6 +1433,25 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         u = roll_force<kFmt>(late_params(), anext, L.agent);
         arow = nrow;
         wave_sync();
+    }
+    // the final state (what the next launch or an eager step reads)
+    KernargParams &q = late_params();
+    if (wave_live) {
+        float2 *const pos_b = q.pos + eb * E;
+        if (L0.lane < E) pos_b[L0.lane] = s_pos[L0.lane];
+        if (L0.lane + kWave < E) pos_b[L0.lane + kWave] = s_pos[L0.lane + kWave];
+        if (L0.agent) {
+            (q.vel + eb * N)[L0.lane] = v;
+            (q.contact_mask + eb * N)[L0.lane] = cand_prev;
+        }
+        if (L0.live) (q.row_mask + eb * M)[L0.lane] = oo;
+        if (L0.lane == 0) {
+            q.step_count[L0.b] = t;
+            q.episode[L0.b] = ep;
+            q.ep_acc[L0.b] = acc;
+            q.edge_count[L0.b] = s_bc[((K - 1) & 1) * kWavesPerBlock + wave];
+            if (q.degenerate) q.degenerate[L0.b] = deg;
+        }
     }
 }
 
