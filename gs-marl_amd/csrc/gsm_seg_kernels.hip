@@ -611,7 +611,11 @@ __device__ __forceinline__ void block_emit(const DevParams &p, const Shape<kN, k
     const int first = blockIdx.x * kWavesPerBlock * s.G;
     // one env per wave, compile-time shape: the env's list is staged in LDS
     // before the prefix exchange (needs only local counts)
+#ifdef GSM_ABL_NOSTAGE   // timing experiment: per-lane row writes only
+    constexpr bool kStaged = false;
+#else
     constexpr bool kStaged = kG == 1 && kN > 0 && kN <= 31 && kNo <= 32;
+#endif
     int staged = -1;
 #ifndef GSM_ABL_NO_ROWS
     if constexpr (kStaged) {
@@ -1393,33 +1397,44 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         // this workgroup's envs are read before block_emit's barrier)
 #ifndef ROLLX_NOEMIT
         if (k > 0) {
-            BlockPrefix pre;
-            pre.cnt_k = L.lane < kWavesPerBlock ? s_bc[(1 - par) * kWavesPerBlock + L.lane] : 0;
-            KernargParams &qe = late_params();
-#ifdef ROLLX_NOPRE
-            pre.acc = 0;
-#else
-            // wave 0 walks back over the predecessors and publishes this
-            // workgroup's inclusive prefix of step t - 1 at once
-            pre.acc = 0;
+            const int *cb = s_bc + (1 - par) * kWavesPerBlock;   // this workgroup's counts of step t - 1
+            // the env's list staged first (needs only its own row counts)
+            const int staged = wave_live ? stage_rows<kN, kNo>(L, (uint32_t *)s_nf, scr_cap, oo) : -1;
+            // wave 0 walks back over the predecessors, hands the workgroup's
+            // offset to the other waves and publishes its inclusive prefix
             if (wave == 0) {
+                KernargParams &qe = late_params();
                 const int64_t kb = (int64_t)(k - 1) * gridDim.x;
+#ifdef ROLLX_NOPRE
+                const int ex = 0;
+#else
                 const int ex = roll_lookback(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
                                              (uint32_t)k, qe.roll.status, L.lane);
-                int own = 0;
-                for (int w = 0; w < kWavesPerBlock; ++w) own += s_bc[(1 - par) * kWavesPerBlock + w];
+#endif
                 if (L.lane == 0) {
-                    pre.acc = ex;
+                    s_red[0] = ex;
                     __hip_atomic_store((gu64 *)(qe.roll.gran + (int64_t)K * gridDim.x + kb + blockIdx.x),
-                                       ((uint64_t)k << 32) | (uint32_t)(ex + own), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
+                                       ((uint64_t)k << 32) | (uint32_t)(ex + cb[0] + cb[1] + cb[2] + cb[3]),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
-#endif
-            KernargParams &qs = late_params();
-            block_emit<kN, kNo, 1>(p, s, L, s_prev, oo, pre, s_red, qs.lag.edge_ptr,
-                                   EdgeSink{qs.lag.edge_index, qs.lag.edge_attr, qs.lag.cap}, (uint32_t *)s_nf,
-                                   scr_cap);
+            __syncthreads();
+            int before = 0;
+            for (int w = 0; w < kWavesPerBlock; ++w) before += w < wave ? cb[w] : 0;
+            const int my_cnt = cb[wave];
+            const int64_t env_off = (int64_t)s_red[0] + before;
+            if (wave_live) {
+                KernargParams &qs = late_params();
+                if (L.lane == 0) {
+                    qs.lag.edge_ptr[L.b] = env_off;
+                    if (L.b == p.B - 1) qs.lag.edge_ptr[p.B] = env_off + my_cnt;
+                }
+                const EdgeSink out{qs.lag.edge_index, qs.lag.edge_attr, qs.lag.cap};
+                if (staged >= 0 && env_off + staged <= out.cap)
+                    write_staged<kN, kNo>(L, s_prev, (uint32_t *)s_nf, staged, env_off, out);
+                else
+                    emit_rows<kN, kNo, 1>(s, L, s_prev, oo, env_off, out, env_off + my_cnt > out.cap);
+            }
             wave_sync();
         }
 #endif
