@@ -7,17 +7,17 @@ owns 8192 envs with global Philox env ids, BASELINE configs[4] at N=8).
 
 A "step" = one env.step of every env on the GPU: action force, pairwise
 contact physics, integration, reward, collision cost, done/auto-reset, node
-features and the packed COO edge list, every output of every step written to
-HBM. Inside a graph the one-env-per-wave segmented configs (the
-headline) run all steps of the episode graph in ONE fused rollout launch
-(GSM_GRAPH_ROLL: env state kept on chip, the CSR prefix handed between
-workgroups in-launch); the other segmented configs one launch per step (step
-j+1's kernel first emits step j's edges); `--no-roll` / `--unfused` select
-those chains instead. Actions
-are pre-generated on device (100 x B x N int32, uniform over the 5 discrete
-actions) so the timed region has no host work; the K timed steps are
-replayed from HIP graphs of one episode (100 steps) each, with the per-episode
-RCCL all-reduce of episode metrics between chunks when N > 1.
+features and the packed COO edge list; every observation output of every step
+is written to HBM. Inside a graph the headline (one env per
+wave) and the tile configs (C3) run all steps of the episode graph in ONE
+fused rollout launch (GSM_GRAPH_ROLL: env state kept on chip, the CSR prefix
+handed between workgroups in-launch), the other segmented configs one launch
+per step (step j+1's kernel first emits step j's edges); `--no-roll` /
+`--unfused` select those chains instead. Actions are pre-generated on device
+(100 x B x N int32, uniform over the 5 discrete actions) so the timed region
+has no host work; the K timed steps are replayed from HIP graphs of one
+episode (100 steps) each, with the per-episode RCCL all-reduce of episode
+metrics between chunks when N > 1.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -96,16 +96,19 @@ def lag_extra_bytes(B, N, No, total_edges, seg=True):
     return B * (masks + 4 + 8) + 12 * total_edges
 
 
-def roll_step_bytes(B, N, No, EL, action_bytes, total_edges):
+def roll_step_bytes(B, N, No, EL, action_bytes, total_edges, seg=True):
     """Algorithmic HBM bytes per step of the fused rollout launch. The
     simulator state (positions, velocities, masks, counters) stays on chip and
     is loaded / stored once per launch (left out: under 1% over 100 steps); a
     step reads its actions and writes its observation outputs: the agent
-    node-feature rows, reward, cost, done, and (one iteration later) the
-    edge_ptr entry and 12 B per edge; at an episode end the static node rows
-    and the episode metrics, amortised over the episode."""
+    node-feature rows (7 floats on the segmented path, 6 on the tile path
+    whose type column is static), reward, cost, done, and (one iteration
+    later) the edge_ptr entry and 12 B per edge; at an episode end the static
+    node rows, amortised over the episode. (The tile path also re-reads its
+    contact words and the previous step's row masks from L2: on-chip traffic
+    of the workgroup's own writes, not counted.)"""
     E = 2 * N + No
-    writes = 28 * N + 4 * N + 4 * N + 1 + 8
+    writes = (28 if seg else 24) * N + 4 * N + 4 * N + 1 + 8
     reset = (28 * (E - N) + 8) / EL
     return B * (action_bytes * N + writes + reset) + 12 * total_edges
 
@@ -604,9 +607,10 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False):
         sb, eb = ragged_kernel_bytes(env, EL, 4, edges_now)
         names = ("gsm_step_ragged_kernel", "gsm_emit_ragged_kernel")
     elif roll:
-        sb = roll_step_bytes(B, N, cfg.n_obstacles, EL, 4, edges_now)
+        sb = roll_step_bytes(B, N, cfg.n_obstacles, EL, 4, edges_now, seg)
         eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)
-        names = (f"gsm_roll_seg_kernel (per step of a {L}-step launch)", "gsm_emit_seg_kernel")
+        fam = "seg" if seg else "tile"
+        names = (f"gsm_roll_{fam}_kernel (per step of a {L}-step launch)", f"gsm_emit_{fam}_kernel")
     else:
         sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4, seg, env.sizes.envs_per_block)
         if lag:

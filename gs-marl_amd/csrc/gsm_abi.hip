@@ -39,6 +39,7 @@ struct gsm_handle {
         uint64_t *gran = nullptr;     // fused rollout: [K][n_blocks] edge-sum granules
     } slots[GSM_GRAPH_SLOTS];
     uint32_t *roll_status = nullptr;  // fused rollout: a bounded wait gave up (sticky until read)
+    uint64_t *roll_rows = nullptr;    // tile rollout: the second row-mask buffer [B][M][W]
 };
 
 namespace {
@@ -512,11 +513,13 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     p.action_fmt = action_fmt;
     p.env_mask = nullptr;
     p.reseed = 0;
-    const void *roll_fn = gsm::roll_seg_kernel_fn(p);
+    const bool tile = p.path == gsm::kPathTile;
+    const void *roll_fn = tile ? gsm::roll_tile_kernel_fn(p) : gsm::roll_seg_kernel_fn(p);
     if (!roll_fn) return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: no fused rollout kernel for this config "
-                                             "(segmented path, one env per wave, compiled shape)");
+                                             "(segmented path with one env per wave and a compiled shape, "
+                                             "or tile path with the symmetric sweep)");
     const int nb = gsm::step_grid_blocks(p);
-    const size_t roll_lds = gsm::roll_kernel_lds(p);
+    const size_t roll_lds = tile ? gsm::roll_tile_kernel_lds(p) : gsm::roll_kernel_lds(p);
     // every workgroup resident at once (one residency round; a workgroup only
     // waits on lower-numbered ones, so this is for speed, not for progress)
     int dev = 0, per_cu = 0, n_cu = 0;
@@ -537,6 +540,10 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     if (!h->cap_stream) {
         e = hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking);
         if (e != hipSuccess) return hip_fail(h, e, "hipStreamCreate");
+    }
+    if (tile && !h->roll_rows) {   // the tile rollout double-buffers the row masks
+        e = hipMalloc(&h->roll_rows, (size_t)p.B * p.M * p.W * sizeof(uint64_t));
+        if (e != hipSuccess) { h->roll_rows = nullptr; return hip_fail(h, e, "hipMalloc (rollout row masks)"); }
     }
     const int K = n_steps;
     // aggregates [K][nb], then inclusive prefixes [K][nb] (look-back)
@@ -576,7 +583,8 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     p.actions = actions;
     p.lag = gsm::DevParams::Lag{p.block_edge_sum, p.edge_count, p.edge_ptr, p.edge_index, p.edge_attr,
                                 p.edge_capacity};
-    p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, 0, sl.gran, h->roll_status};
+    p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, 0, sl.gran, h->roll_status,
+                                  h->roll_rows};
     if (e == hipSuccess) {
         what = "rollout kernel node";
         hipKernelNodeParams kp = {};
@@ -863,6 +871,7 @@ int gsm_destroy(gsm_handle *h) {
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->bsum_alt) (void)hipFree(h->bsum_alt);
     if (h->roll_status) (void)hipFree(h->roll_status);
+    if (h->roll_rows) (void)hipFree(h->roll_rows);
     if (h->order_copied) (void)hipEventSynchronize(h->order_copied);
     if (h->block_order) (void)hipFree(h->block_order);
     if (h->order_host) (void)hipHostFree(h->order_host);

@@ -215,4 +215,52 @@ __device__ __forceinline__ float contact_scale(const Params &p, float d2, float 
     return p.cf * pen * __builtin_amdgcn_rcpf(d);
 }
 
+// ---- fused rollout hand-offs (gsm_seg_kernels.hip / gsm_tile_kernels.hip)
+typedef __attribute__((address_space(1))) uint64_t gu64;
+typedef __attribute__((address_space(1))) uint32_t gu32;
+constexpr uint64_t kRollSpinTicks = 20000000ull;   // s_memrealtime ticks (100 MHz): 0.2 s
+
+// one granule, polled until its tag matches (cold path)
+__device__ __forceinline__ uint64_t roll_wait(const uint64_t *g, uint32_t tag, uint32_t *status) {
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        const uint64_t x = __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((uint32_t)(x >> 32) == tag) return x;
+        if (__hip_atomic_load((gu32 *)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
+            __builtin_amdgcn_s_memrealtime() - t0 > kRollSpinTicks) {
+            __hip_atomic_store((gu32 *)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return (uint64_t)tag << 32;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+
+// Decoupled look-back over the preceding workgroups (ONE wave; wave-uniform
+// result): windows of 64 predecessors, nearest first; the nearest one whose
+// inclusive prefix is published ends the walk (its inclusive + the aggregates
+// of those in between), otherwise the window's aggregates are added and the
+// walk moves on. Aggregates were published an iteration earlier, so the walk
+// never waits on an inclusive prefix; an aggregate read early is re-polled.
+__device__ __forceinline__ int roll_lookback(const uint64_t *agg_k, const uint64_t *inc_k, uint32_t tag,
+                                             uint32_t *status, int lane) {
+    int acc = 0;
+    for (int hi = (int)blockIdx.x; hi > 0; hi -= kWave) {
+        const int idx = hi - 1 - lane;                      // lane 0 = nearest predecessor
+        const int ci = idx >= 0 ? idx : 0;
+        const uint64_t xi = __hip_atomic_load((const gu64 *)(inc_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t xa = __hip_atomic_load((const gu64 *)(agg_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool valid = idx >= 0;
+        const uint64_t have = __ballot(valid && (uint32_t)(xi >> 32) == tag);
+        const int j = have ? __builtin_ctzll(have) : kWave;   // wave-uniform
+        // aggregates of lanes < j (all valid lanes when no inclusive was found)
+        const bool need = valid && lane < j;
+        if (need && (uint32_t)(xa >> 32) != tag) xa = roll_wait(agg_k + ci, tag, status);
+        int v = need ? (int)(uint32_t)xa : 0;
+        if (lane == j) v = (int)(uint32_t)xi;
+        acc += wave_total(v);
+        if (have) break;
+    }
+    return acc;
+}
+
 }  // namespace gsm

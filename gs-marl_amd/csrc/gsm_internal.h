@@ -99,6 +99,7 @@ struct DevParams {
         int32_t n_actions, t_first, K, pad;
         uint64_t *gran;
         uint32_t *status;
+        uint64_t *rows_alt;   // tile path: [B][M][W] row masks of every other step (double buffer)
     } roll;
 };
 
@@ -128,6 +129,8 @@ const void *emit_seg_kernel_fn(const DevParams &p);
 // runtime shapes, other families) and its LDS bytes
 const void *roll_seg_kernel_fn(const DevParams &p);
 size_t roll_kernel_lds(const DevParams &p);
+const void *roll_tile_kernel_fn(const DevParams &p);   // nullptr unless p.tile_sym
+size_t roll_tile_kernel_lds(const DevParams &p);
 const void *step_ragged_kernel_fn();
 const void *step_tile_kernel_fn();
 const void *emit_tile_kernel_fn();

@@ -191,8 +191,12 @@ __device__ __forceinline__ uint64_t agent_bits_of_word(int N, int k) {   // agen
     return N <= lo ? 0ull : (N >= lo + 64 ? ~0ull : ((1ull << (N - lo)) - 1ull));
 }
 
+// rout: where the row masks go; rkeep: where the cached obstacle-obstacle
+// words are read (keep_oo) — the same buffer except in the fused rollout,
+// which double-buffers the masks (the previous step's are emitted later)
 __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s_pos, const TileSymLds &S,
-                                             int *s_cost, int64_t eb, bool keep_oo) {
+                                             int *s_cost, int64_t eb, bool keep_oo, uint64_t *rout = nullptr,
+                                             const uint64_t *rkeep = nullptr) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     const int N = p.N, M = p.M, W = p.W, No = p.No;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -249,7 +253,9 @@ __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s
         if (obst) ((uint8_t *)(S.own + (int64_t)(m - N) * W))[jb] = (uint8_t)(__builtin_bitreverse32(own) >> (32 - nc));
     }
     __syncthreads();
-    uint64_t *const rmask = p.row_mask + eb * M * W;
+    uint64_t *const rmask = rout ? rout : p.row_mask + eb * M * W;
+    const uint64_t *const rprev = rkeep ? rkeep : rmask;
+    const bool rewrite = rprev != rmask;                    // every word is written
     uint64_t *const cmask = p.contact_mask + eb * N * W;
     int pairs = 0, coinc = 0;
     for (int r = tid; r < M; r += kTileBlock) {
@@ -285,7 +291,7 @@ __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s
                 const uint64_t am = agent_bits_of_word(N, k);
                 uint64_t oo = 0;
                 if (keep_oo) {
-                    oo = rmask[(int64_t)r * W + k] & ~am;   // obstacle-obstacle bits: static in an episode
+                    oo = rprev[(int64_t)r * W + k] & ~am;   // obstacle-obstacle bits: static in an episode
                 } else {
                     const int c1 = min(64 * k + 64, M);
                     for (int ci = max(64 * k, N); ci < c1; ++ci) {
@@ -296,7 +302,7 @@ __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s
                     }
                 }
                 const uint64_t w = (ow[k] & am) | oo;
-                if (am || !keep_oo) rmask[(int64_t)r * W + k] = w;
+                if (am || !keep_oo || rewrite) rmask[(int64_t)r * W + k] = w;
                 pairs += __popcll(w);
             }
         }
@@ -754,6 +760,291 @@ __global__ __launch_bounds__(kTileBlock) void gsm_emit_tile_kernel(DevParams p) 
         p.edge_ptr[b] = off;
         if (b == p.B - 1) p.edge_ptr[p.B] = off + p.edge_count[b];
     }
+}
+
+// ---------------------------------------------------------------------------
+// Fused rollout on the tile path (one 512-thread workgroup per env; C3):
+// K steps of a graph in one launch, as gsm_roll_seg_kernel.
+// Positions and velocities stay in LDS; contact masks are re-read from global
+// memory written by this workgroup's previous sweep (a workgroup barrier
+// orders them); the row masks alternate between the bound buffer and
+// p.roll.rows_alt (step k writes slot (K-1-k) & 1, so the last step's masks
+// land in the bound buffer for the emit launch that follows), so step k-1's
+// masks survive step k's sweep and are emitted after it at the offset found
+// by the look-back over per-env granules (one env per workgroup). The step's
+// outputs (node features, reward, cost, done) are written every step, the
+// state once after the loop. Same operations as gsm_step_tile_kernel in the
+// same order: bit-identical outputs.
+constexpr int kRollTileScr = 2048;   // staged edge words (C3: ~390 edges per env; else direct writes)
+
+size_t roll_tile_kernel_lds(const DevParams &p) {
+    return (size_t)p.wave_lds_step + 8 * (size_t)p.E + 16 + 8 * kTileWaves + 4 * kRollTileScr;
+}
+
+template <typename Params>
+__device__ __forceinline__ float2 roll_tile_force(const Params &p, int row, int64_t a) {
+    const char *base = p.roll.actions + (int64_t)row * p.roll.stride;
+    float ux, uy;
+    if (p.action_fmt == 0) {
+        const float *q = (const float *)base + a * 5;
+        ux = q[1] - q[2];
+        uy = q[3] - q[4];
+    } else if (p.action_fmt == 1) {
+        const int k = ((const int32_t *)base)[a];
+        ux = (float)(k == 1) - (float)(k == 2);
+        uy = (float)(k == 3) - (float)(k == 4);
+    } else {
+        const float2 q = ((const float2 *)base)[a];
+        ux = q.x;
+        uy = q.y;
+    }
+    return make_float2(ux * p.sens, uy * p.sens);
+}
+
+__global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel(DevParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int b = blockIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int N = p.N, E = p.E, W = p.W, M = p.M;
+    float2 *s_pos = (float2 *)smem;           // [E]
+    float2 *s_vel = s_pos + E;                // [N]
+    float2 *s_np = s_vel + N;                 // [N] integrated agent positions
+    int *s_cost = (int *)(s_np + N);          // [N]
+    int *s_ired = s_cost + N;                 // [4 * kTileWaves] reduction slots
+    float *s_fred = (float *)(s_ired + 4 * kTileWaves);
+    int *s_deg = (int *)(s_fred + kTileWaves);   // [2] (unsymmetric sweep's coincident flag), unused here
+    TileSymLds sym;
+    {
+        unsigned char *q = smem + ((8 * E + 8 * N + 8 * N + 4 * N + 20 * kTileWaves + 8 + 15) & ~15);
+        sym.xy = (float *)q;
+        q += 16 * ((N + 1) / 2);
+        sym.arow = (uint64_t *)q;
+        q += 16 * N * W;
+        sym.own = (uint64_t *)q;
+        q += 8 * p.No * W;
+        sym.flag = (int *)q;
+    }
+    float2 *s_prev = (float2 *)(smem + p.wave_lds_step);   // [E] positions of the previous step
+    int *s_x = (int *)(s_prev + E);                        // [4]
+    int *s_red = s_x + 4;                                  // [2 * kTileWaves] emit_env exchange
+    uint32_t *s_scr = (uint32_t *)(s_red + 2 * kTileWaves);
+    const int64_t eb = b;
+    const int32_t g0 = (int32_t)(eb * E);
+    uint64_t *const rbuf[2] = {p.row_mask + eb * M * W, p.roll.rows_alt + eb * M * W};
+
+    for (int e = tid; e < E; e += kTileBlock) s_pos[e] = p.pos[eb * E + e];
+    for (int i = tid; i < N; i += kTileBlock) s_vel[i] = p.vel[eb * N + i];
+    int t = p.step_count[b];
+    int ep = p.episode[b];
+    float2 acc = p.ep_acc[b];
+    if (tid == 0) s_deg[0] = s_deg[1] = 0;
+    const int K = p.roll.K, n_act = p.roll.n_actions;
+    int arow = p.roll.t_first % n_act;
+    int prev_edges = 0, bad = 0;
+    __syncthreads();
+
+    for (int k = 0; k < K; ++k) {
+        uint64_t *const rout = rbuf[(K - 1 - k) & 1];
+        const uint64_t *const rkeep = k == 0 ? rbuf[0] : rbuf[(K - k) & 1];   // the previous step's masks
+        bool relaid = false;
+        auto relayout = [&]() {   // scenario.reset_world with the Philox layout
+            ep = ep + 1;
+            t = 0;
+            acc = make_float2(0.0f, 0.0f);
+            const uint32_t gid = (uint32_t)(p.env_base + b);
+            __syncthreads();
+            for (int e = tid; e < E; e += kTileBlock) s_pos[e] = layout_pos(p, gid, (uint32_t)ep, (uint32_t)e);
+            for (int i = tid; i < N; i += kTileBlock) s_vel[i] = make_float2(0.0f, 0.0f);
+            relaid = true;
+            __syncthreads();
+        };
+        // apply_environment_force + integrate_state (as gsm_step_tile_kernel)
+        const uint64_t *cm = late_params().contact_mask + eb * N * W;
+        for (int i = tid; i < N; i += kTileBlock) {
+            const float2 pi = s_pos[i];
+            const float2 u = roll_tile_force(late_params(), arow, eb * N + i);
+            float fx = 0.0f, fy = 0.0f;
+            for (int kw = 0; kw < W; ++kw) {
+                uint64_t bits = cm[(int64_t)i * W + kw];
+                while (bits) {
+                    const int c = 64 * kw + __builtin_ctzll(bits);
+                    bits &= bits - 1;
+                    const bool ag = c < N;
+                    const float2 pj = s_pos[collider_entity(c, N)];
+                    const float dx = pi.x - pj.x, dy = pi.y - pj.y;
+                    const float d2 = dx * dx + dy * dy;
+                    const float f = contact_scale(p, d2, ag ? p.dmin_aa : p.dmin_ao);
+                    fx += f * dx;
+                    fy += f * dy;
+                }
+            }
+            float Fx = u.x + fx, Fy = u.y + fy;
+            if (p.strict && strict_bad(i, pi, N, p.M, [&](int c) { return s_pos[collider_entity(c, N)]; })) {
+                Fx = __builtin_nanf("");
+                Fy = __builtin_nanf("");
+            }
+            float2 v = s_vel[i];
+            v.x = v.x * p.omd;
+            v.y = v.y * p.omd;
+            v.x = v.x + (Fx / p.mass) * p.dt;
+            v.y = v.y + (Fy / p.mass) * p.dt;
+            if (p.max_speed > 0.0f) {
+                const float sp = sqrtf(v.x * v.x + v.y * v.y);
+                if (sp > p.max_speed) {
+                    v.x = v.x / sp * p.max_speed;
+                    v.y = v.y / sp * p.max_speed;
+                }
+            }
+            s_vel[i] = v;
+            s_np[i] = make_float2(pi.x + v.x * p.dt, pi.y + v.y * p.dt);
+        }
+        __syncthreads();
+        for (int i = tid; i < N; i += kTileBlock) s_pos[i] = s_np[i];
+        __syncthreads();
+        t += 1;
+        const bool done = t >= p.EL;
+
+        int pairs = obs_sweep_sym(p, s_pos, sym, s_cost, eb, true, rout, rkeep);
+        auto nonfinite_part = [&]() {
+            int bd = 0;
+            if (p.degenerate)
+                for (int i = tid; i < N; i += kTileBlock) bd |= nonfinite2(s_pos[i]) ? 1 : 0;
+            return bd;
+        };
+        float rpart = 0.0f;
+        for (int i = tid; i < N; i += kTileBlock) {
+            const float2 a = s_pos[i], g = s_pos[N + i];
+            const float dx = a.x - g.x, dy = a.y - g.y;
+            rpart += -sqrtf(dx * dx + dy * dy);
+        }
+        __syncthreads();
+        int cpart = 0;
+        for (int i = tid; i < N; i += kTileBlock) {
+            const int cnt = s_cost[i];
+            late_params().cost[eb * N + i] = (float)cnt;
+            cpart += cnt;
+            if (!p.shared_reward) {
+                const float2 a = s_pos[i], g = s_pos[N + i];
+                const float dx = a.x - g.x, dy = a.y - g.y;
+                late_params().reward[eb * N + i] = -sqrtf(dx * dx + dy * dy);
+            }
+        }
+        {
+            const float rw = wave_total(rpart);
+            const int cw = wave_total(cpart), pw = wave_total(pairs), bw = wave_total(nonfinite_part());
+            if (lane == 0) {
+                s_fred[wave] = rw;
+                s_ired[wave] = cw;
+                s_ired[kTileWaves + wave] = pw;
+                s_ired[2 * kTileWaves + wave] = bw;
+            }
+        }
+        __syncthreads();
+        float rsum = 0.0f;
+        int csum = 0;
+        bad = 0;
+        pairs = 0;
+#pragma unroll
+        for (int w = 0; w < kTileWaves; ++w) {
+            rsum += s_fred[w];
+            csum += s_ired[w];
+            pairs += s_ired[kTileWaves + w];
+            bad |= s_ired[2 * kTileWaves + w];
+        }
+        if (p.shared_reward) {
+            for (int i = tid; i < N; i += kTileBlock) late_params().reward[eb * N + i] = rsum;
+            rsum *= (float)N;
+        }
+        acc.x += rsum;
+        acc.y += (float)csum;
+        if (done && p.auto_reset) {
+            if (tid == 0) late_params().ep_last[b] = acc;
+            relayout();
+            pairs = obs_sweep_sym(p, s_pos, sym, s_cost, eb, false, rout, rkeep);
+            pairs = tile_sum(pairs, s_ired);
+            bad = tile_sum(nonfinite_part(), s_ired + 3 * kTileWaves);
+        }
+        // the step's observation outputs: agent node rows, static rows on a new layout
+        float *nf = late_params().node_feat + eb * E * 7;
+        const bool full = relaid || p.nf_full;
+        for (int i = tid; i < N; i += kTileBlock) {
+            const float2 v = s_vel[i], a = s_pos[i], g = s_pos[N + i];
+            float *row = nf + (int64_t)i * 7;
+            row[0] = v.x;
+            row[1] = v.y;
+            row[2] = a.x;
+            row[3] = a.y;
+            row[4] = g.x - a.x;
+            row[5] = g.y - a.y;
+            if (full) row[6] = 0.0f;
+        }
+        if (full) {
+            for (int e = N + tid; e < E; e += kTileBlock) {
+                const float2 a = s_pos[e];
+                float *row = nf + (int64_t)e * 7;
+                row[0] = 0.0f;
+                row[1] = 0.0f;
+                row[2] = a.x;
+                row[3] = a.y;
+                row[4] = 0.0f;
+                row[5] = 0.0f;
+                row[6] = e < 2 * N ? 1.0f : 2.0f;
+            }
+        }
+        const int edges = pairs + 2 * N;   // directed radius edges + agent<->goal
+        if (tid == 0) {
+            KernargParams &q = late_params();
+            q.done[b] = done ? 1 : 0;
+            __hip_atomic_store((gu64 *)(q.roll.gran + (int64_t)k * gridDim.x + b),
+                               ((uint64_t)(k + 1) << 32) | (uint32_t)edges, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+        // the previous step's edges at the offset of the look-back
+        if (k > 0) {
+            int ex = 0;
+            if (wave == 0) {
+                const int64_t kb = (int64_t)(k - 1) * gridDim.x;
+                KernargParams &q = late_params();
+                ex = roll_lookback(q.roll.gran + kb, q.roll.gran + (int64_t)K * gridDim.x + kb, (uint32_t)k,
+                                   q.roll.status, lane);
+                if (lane == 0)
+                    __hip_atomic_store((gu64 *)(late_params().roll.gran + (int64_t)K * gridDim.x + kb + b),
+                                       ((uint64_t)k << 32) | (uint32_t)(ex + prev_edges), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+            int64_t off;
+            {
+                KernargParams &q = late_params();
+                emit_env(p, EdgeSink{q.edge_index, q.edge_attr, q.edge_capacity}, s_prev, rkeep, tid == 0 ? ex : 0,
+                         &off, s_red, s_scr, kRollTileScr, g0);
+            }
+            if (tid == 0) {
+                KernargParams &q = late_params();
+                q.edge_ptr[b] = off;
+                if (b == p.B - 1) q.edge_ptr[p.B] = off + prev_edges;
+            }
+        }
+        __syncthreads();   // s_prev and the staged words read
+        for (int e = tid; e < E; e += kTileBlock) s_prev[e] = s_pos[e];
+        prev_edges = edges;
+        arow = arow + 1 == n_act ? 0 : arow + 1;
+        __syncthreads();
+    }
+    // the final state (what the next launch or an eager step reads)
+    for (int e = tid; e < E; e += kTileBlock) p.pos[eb * E + e] = s_pos[e];
+    for (int i = tid; i < N; i += kTileBlock) p.vel[eb * N + i] = s_vel[i];
+    if (tid == 0) {
+        p.step_count[b] = t;
+        p.episode[b] = ep;
+        p.ep_acc[b] = acc;
+        p.edge_count[b] = prev_edges;
+        p.block_edge_sum[b] = prev_edges;
+        if (p.degenerate) p.degenerate[b] = (uint8_t)((*sym.flag ? kDegCoincident : 0) | (bad ? kDegNonfinite : 0));
+    }
+}
+
+const void *roll_tile_kernel_fn(const DevParams &p) {
+    return p.path == kPathTile && p.tile_sym ? reinterpret_cast<const void *>(&gsm_roll_tile_kernel) : nullptr;
 }
 
 const void *step_tile_kernel_fn() { return reinterpret_cast<const void *>(&gsm_step_tile_kernel); }

@@ -4,8 +4,9 @@ other through tagged granules. Every state and output buffer must equal the
 eager steps' (which test_gpu_parity checks against the oracle) bit for bit:
 partial workgroups, auto-resets (episode length 5 and 7), all three action
 formats, repeated replays (the granules are re-zeroed by the graph), and the
-headline batch (one residency round of 2048 workgroups). Also checked against
-the CPU oracle directly at the end of a chain."""
+headline batch (one residency round of 2048 workgroups), and the tile path's
+rollout (one 512-thread workgroup per env, C3's 96 agents). Also checked
+against the CPU oracle directly at the end of a chain."""
 import numpy as np
 import pytest
 import torch
@@ -51,13 +52,17 @@ def _same(ref, env, what):
     assert torch.equal(ref["edge_attr"][:n], env.t["edge_attr"][:n]), what
 
 
-@pytest.mark.parametrize("B,T,EL,fmt", [(64, 12, 5, "index"), (257, 9, 7, "index"), (8, 2, 5, "index"), (40, 1, 5, "index"),
-                                        (130, 11, 5, "onehot"), (99, 8, 3, "cont"), (8192, 26, 25, "index")])
-def test_roll_equals_eager(B, T, EL, fmt):
-    env, cfg = _env(n_agents=24, n_envs=B, episode_length=EL)
+@pytest.mark.parametrize("N,B,T,EL,fmt", [(24, 64, 12, 5, "index"), (24, 257, 9, 7, "index"), (24, 8, 2, 5, "index"),
+                                          (24, 40, 1, 5, "index"), (24, 130, 11, 5, "onehot"), (24, 99, 8, 3, "cont"),
+                                          (24, 8192, 26, 25, "index"),
+                                          # tile path (one workgroup per env): C3's shape
+                                          (96, 16, 9, 5, "index"), (96, 33, 6, 4, "onehot"), (96, 7, 5, 2, "cont"),
+                                          (96, 1024, 12, 10, "index"), (70, 9, 3, 2, "index")])
+def test_roll_equals_eager(N, B, T, EL, fmt):
+    env, cfg = _env(n_agents=N, n_envs=B, episode_length=EL)
     gen = torch.Generator(device=DEV)
     gen.manual_seed(B * 31 + T)
-    acts = _actions(fmt, max(T - 3, 1), B, 24, gen)   # fewer action rows than steps: the ring wraps
+    acts = _actions(fmt, max(T - 3, 1), B, N, gen)   # fewer action rows than steps: the ring wraps
     ref = _eager(env, acts, T, seed=11)
     env.reset(seed=11)
     env.capture(acts, T, slot=0, kernels="roll")
@@ -83,12 +88,13 @@ def test_roll_equals_eager(B, T, EL, fmt):
     env.close()
 
 
-def test_roll_emit_after_chain():
+@pytest.mark.parametrize("N,B", [(24, 300), (96, 20)])
+def test_roll_emit_after_chain(N, B):
     """The bound edge-sum half holds the last step's sums after a rollout
     graph: an emit-only graph right after it re-emits the same edges."""
-    B, T = 300, 10
-    env, cfg = _env(n_agents=24, n_envs=B, episode_length=6)
-    acts = torch.randint(0, 5, (T, B, 24), dtype=torch.int32, device=DEV)
+    T = 10
+    env, cfg = _env(n_agents=N, n_envs=B, episode_length=6)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
     ref = _eager(env, acts, T, seed=4)
     env.reset(seed=4)
     env.capture(acts, T, slot=1, kernels="roll")
@@ -101,16 +107,17 @@ def test_roll_emit_after_chain():
     env.close()
 
 
-def test_roll_oracle_direct():
+@pytest.mark.parametrize("N,B", [(24, 48), (96, 12)])
+def test_roll_oracle_direct(N, B):
     """The last step of a rollout graph vs the fp64 CPU oracle stepped from
     the identical fp32 pre-step state (eager steps reach it bit for bit):
     positions/velocities within the 1e-6 bar, counters, costs and the CSR
     edges exact (fp32-mode oracle on the kernel's own positions). Episode
     length 6 puts an auto-reset inside the launch."""
-    B, T = 48, 9
-    env, cfg = _env(n_agents=24, n_envs=B, episode_length=6, seed=21)
+    T = 9
+    env, cfg = _env(n_agents=N, n_envs=B, episode_length=6, seed=21)
     ocfg = br.make_cfg(**{k: v for k, v in cfg.to_dict().items() if k in br.DEFAULTS})
-    acts = torch.randint(0, 5, (T, B, 24), dtype=torch.int32, device=DEV)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
     env.reset(seed=21)
     for t in range(T - 1):
         env.step(acts[t], sync_edges=False)
