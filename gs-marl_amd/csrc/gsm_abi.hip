@@ -516,9 +516,10 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     const bool tile = p.path == gsm::kPathTile;
     const void *roll_fn = tile ? gsm::roll_tile_kernel_fn(p) : gsm::roll_seg_kernel_fn(p);
     if (!roll_fn) return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: no fused rollout kernel for this config "
-                                             "(segmented path with one env per wave and a compiled shape, "
-                                             "or tile path with the symmetric sweep)");
-    const int nb = gsm::step_grid_blocks(p);
+                                             "(segmented path with a compiled shape, or tile path with the "
+                                             "symmetric sweep)");
+    // segmented rollout: one env per wave whatever the config's G (4 per workgroup)
+    const int nb = tile ? gsm::step_grid_blocks(p) : (p.B + gsm::kWavesPerBlock - 1) / gsm::kWavesPerBlock;
     const size_t roll_lds = tile ? gsm::roll_tile_kernel_lds(p) : gsm::roll_kernel_lds(p);
     // every workgroup resident at once (one residency round; a workgroup only
     // waits on lower-numbered ones, so this is for speed, not for progress)
@@ -546,11 +547,16 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         if (e != hipSuccess) { h->roll_rows = nullptr; return hip_fail(h, e, "hipMalloc (rollout row masks)"); }
     }
     const int K = n_steps;
-    // aggregates [K][nb], then inclusive prefixes [K][nb] (look-back)
-    const size_t gran_bytes = 2 * (size_t)K * nb * sizeof(uint64_t);
-    const size_t gran_alloc = (gran_bytes + 15) & ~(size_t)15;
+    if (K > 65535) return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: n_steps must be <= 65535");
+    // a 16-byte header (the launch epoch), then aggregates [K][nb] and
+    // inclusive prefixes [K][nb] (look-back); zeroed once here — granules are
+    // tagged with the launch epoch, so replays never clear them
+    const size_t gran_alloc = 16 + 2 * (size_t)K * nb * sizeof(uint64_t);
     e = hipMalloc(&sl.gran, gran_alloc);
     if (e != hipSuccess) { sl.gran = nullptr; return hip_fail(h, e, "hipMalloc (rollout granules)"); }
+    e = hipMemsetAsync(sl.gran, 0, gran_alloc, h->cap_stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(h->cap_stream);
+    if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipMemset (rollout granules)"); }
     const bool ends = (flags & GSM_GRAPH_TIME_ENDS) != 0;
     sl.events.resize(ends ? 2 : 0, nullptr);
     for (auto &ev : sl.events) {
@@ -560,20 +566,10 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     e = hipGraphCreate(&sl.graph, 0);
     if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipGraphCreate"); }
     hipGraphNode_t prev = nullptr;
-    const char *what = "memset node";
-    {
-        hipMemsetParams mp = {};
-        mp.dst = sl.gran;
-        mp.elementSize = 4;
-        mp.width = gran_alloc / 4;
-        mp.height = 1;
-        mp.pitch = gran_alloc;
-        mp.value = 0;
-        e = hipGraphAddMemsetNode(&prev, sl.graph, nullptr, 0, &mp);
-    }
+    const char *what = "event node";
     auto add_event = [&](hipEvent_t ev) -> hipError_t {
         hipGraphNode_t n;
-        const hipError_t r = hipGraphAddEventRecordNode(&n, sl.graph, &prev, 1, ev);
+        const hipError_t r = hipGraphAddEventRecordNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0, ev);
         if (r == hipSuccess) prev = n;
         return r;
     };
@@ -583,8 +579,8 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     p.actions = actions;
     p.lag = gsm::DevParams::Lag{p.block_edge_sum, p.edge_count, p.edge_ptr, p.edge_index, p.edge_attr,
                                 p.edge_capacity};
-    p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, 0, sl.gran, h->roll_status,
-                                  h->roll_rows};
+    p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, 0, sl.gran + 2, h->roll_status,
+                                  h->roll_rows, (uint32_t *)sl.gran};
     if (e == hipSuccess) {
         what = "rollout kernel node";
         hipKernelNodeParams kp = {};
@@ -596,7 +592,7 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         kp.kernelParams = args;
         kp.extra = nullptr;
         hipGraphNode_t n;
-        e = hipGraphAddKernelNode(&n, sl.graph, &prev, 1, &kp);
+        e = hipGraphAddKernelNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0, &kp);
         if (e == hipSuccess) prev = n;
     }
     if (e == hipSuccess && ends) { what = "event node"; e = add_event(sl.events[1]); }
@@ -611,7 +607,7 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         kp.kernelParams = args;
         kp.extra = nullptr;
         hipGraphNode_t n;
-        e = hipGraphAddKernelNode(&n, sl.graph, &prev, 1, &kp);
+        e = hipGraphAddKernelNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0, &kp);
         if (e == hipSuccess) prev = n;
     }
     if (e != hipSuccess) {

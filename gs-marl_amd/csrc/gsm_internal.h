@@ -91,8 +91,11 @@ struct DevParams {
     // step t_first + k with the actions at actions + ((t_first + k) %
     // n_actions) * stride and emits the previous step's edges into p.lag's
     // outputs; the CSR prefix of step t crosses workgroups through `gran`
-    // ({tag = k + 1, workgroup edge sum} 8-byte granules, [K][grid], zeroed
-    // before every launch). `status` is set when a bounded wait gave up.
+    // (8-byte {tag, workgroup edge sum} granules, aggregates [K][grid] then
+    // inclusive prefixes [K][grid]; tag = epoch << 16 | (k + 1), the launch
+    // epoch read from `*epoch` at launch start and advanced by the emit launch
+    // that ends the graph, so no granule is ever cleared between launches).
+    // `status` is set when a bounded wait gave up.
     struct Roll {
         const char *actions;
         int64_t stride;
@@ -100,6 +103,7 @@ struct DevParams {
         uint64_t *gran;
         uint32_t *status;
         uint64_t *rows_alt;   // tile path: [B][M][W] row masks of every other step (double buffer)
+        uint32_t *epoch;      // nullptr outside rollout graphs (the emit kernel then leaves it)
     } roll;
 };
 

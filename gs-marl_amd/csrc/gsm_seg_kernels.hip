@@ -1099,6 +1099,9 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
     block_emit<kN, kNo, kG>(p, s, L, s_pos, mask, pre, s_red, p.edge_ptr,
                             EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity}, (uint32_t *)(s_pos + E),
                             (p.wave_lds_emit - 8 * G * E) / 4);
+    // the emit launch that ends a rollout graph advances the graph's granule
+    // epoch (the rollout launch has completed; the next one reads it)
+    if (p.roll.epoch && blockIdx.x == 0 && threadIdx.x == 0) *p.roll.epoch = (*p.roll.epoch + 1u) & 0xffffu;
     GSM_STAMP(p, wid, 4);
     GSM_RSTAMP(p, wid, 9);
 }
@@ -1166,11 +1169,22 @@ __device__ __forceinline__ float2 roll_force(const Params &p, float4 a, bool age
 
 template <int kN, int kNo, int kFmt>
 __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevParams p) {
-    static_assert(envs_per_wave<kN, kNo>() == 1 && kFmt >= 0, "one env per wave, compile-time shape");
+    static_assert(kN > 0 && kN <= 31 && kNo <= 32 && kFmt >= 0, "compile-time shape, staged emission");
     constexpr int N = kN, M = kN + kNo, E = 2 * kN + kNo;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Shape<kN, kNo> s(p);
-    const Lane L0 = seg_lane(p, s);
+    // one env per wave whatever the config's G (the step kernels may pack
+    // several small envs into a wave; here a wave's latency chain per step is
+    // the bound, so one env each)
+    Lane L0;
+    L0.wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    L0.lane = threadIdx.x & 63;
+    L0.seg = 0;
+    L0.base = 0;
+    L0.m = L0.lane;
+    L0.b = blockIdx.x * kWavesPerBlock + L0.wave;
+    L0.live = L0.lane < M && L0.b < p.B;
+    L0.agent = L0.live && L0.m < N;
     const int wave = L0.wave;
     const int wstride = p.wave_lds_step + 8 * E;            // + the previous step's positions
     unsigned char *wave_lds = smem + wave * wstride;
@@ -1197,6 +1211,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     wave_sync();
 
     const int K = p.roll.K, n_act = p.roll.n_actions;
+    const uint32_t etag = *p.roll.epoch << 16;              // this launch's tag base
     int arow = p.roll.t_first % n_act;                      // action row of the current step
     uint8_t deg = 0;                                        // App. A S16 flags of the final state
     for (int k = 0; k < K; ++k) {
@@ -1343,11 +1358,34 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             int sum = 0;
             for (int w = 0; w < kWavesPerBlock; ++w) sum += s_bc[par * kWavesPerBlock + w];
             __hip_atomic_store((gu64 *)(q.roll.gran + (int64_t)k * gridDim.x + blockIdx.x),
-                               ((uint64_t)(k + 1) << 32) | (uint32_t)sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (k == K - 1) q.block_edge_sum[blockIdx.x] = sum;   // read by the emit launch that follows
+                               ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)sum, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            // the last step's sums for the emit launch that follows, in the
+            // config's workgroup layout: with G envs per wave the last of the
+            // G rollout workgroups of a slot adds the others' granules
+            if (k == K - 1) {
+                const int G = p.G, r = (int)blockIdx.x;
+                if (G == 1) {
+                    q.block_edge_sum[r] = sum;
+                } else {
+                    const int first = (r / G) * G, last = min(first + G, (int)gridDim.x) - 1;
+                    if (r == last) {
+                        const uint64_t *gk = q.roll.gran + (int64_t)k * gridDim.x;
+                        const uint32_t tag = etag | (uint32_t)(k + 1);
+                        int tot = sum;
+                        for (int j = first; j < r; ++j) {
+                            uint64_t x = __hip_atomic_load((const gu64 *)(gk + j), __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+                            if ((uint32_t)(x >> 32) != tag) x = roll_wait(gk + j, tag, q.roll.status);
+                            tot += (int)(uint32_t)x;
+                        }
+                        q.block_edge_sum[r / G] = tot;
+                    }
+                }
+            }
         }
         // the edges of step t - 1 (kept positions and row masks; the counts of
-        // this workgroup's envs are read before block_emit's barrier)
+        // this workgroup's envs are read before the exchange barrier)
 #ifndef ROLLX_NOEMIT
         if (k > 0) {
             const int *cb = s_bc + (1 - par) * kWavesPerBlock;   // this workgroup's counts of step t - 1
@@ -1362,12 +1400,13 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
                 const int ex = 0;
 #else
                 const int ex = roll_lookback(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
-                                             (uint32_t)k, qe.roll.status, L.lane);
+                                             etag | (uint32_t)k, qe.roll.status, L.lane);
 #endif
                 if (L.lane == 0) {
                     s_red[0] = ex;
                     __hip_atomic_store((gu64 *)(qe.roll.gran + (int64_t)K * gridDim.x + kb + blockIdx.x),
-                                       ((uint64_t)k << 32) | (uint32_t)(ex + cb[0] + cb[1] + cb[2] + cb[3]),
+                                       ((uint64_t)(etag | (uint32_t)k) << 32) |
+                                           (uint32_t)(ex + cb[0] + cb[1] + cb[2] + cb[3]),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
@@ -1375,7 +1414,11 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             int before = 0;
             for (int w = 0; w < kWavesPerBlock; ++w) before += w < wave ? cb[w] : 0;
             const int my_cnt = cb[wave];
-            const int64_t env_off = (int64_t)s_red[0] + before;
+            int64_t env_off = (int64_t)s_red[0] + before;
+            if (env_off < 0 || env_off > p.lag.cap) {   // a broken hand-off: never write out of bounds
+                if (L.lane == 0) __hip_atomic_store((gu32 *)p.roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                env_off = p.lag.cap;
+            }
             if (wave_live) {
                 KernargParams &qs = late_params();
                 if (L.lane == 0) {
@@ -1427,7 +1470,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
 // collectives for 24 agents) and action formats; anything else runs the
 // runtime-shape instantiation.
 #define GSM_SEG_SHAPES(X) X(3, 3) X(24, 24)
-#define GSM_ROLL_SHAPES(X) X(24, 24)   // one env per wave
+#define GSM_ROLL_SHAPES(X) X(3, 3) X(24, 24)
 
 template <bool LAG>
 static const void *pick_step_seg(const DevParams &p) {
@@ -1449,7 +1492,7 @@ const void *lag_step_seg_kernel_fn(const DevParams &p) { return pick_step_seg<tr
 const void *roll_seg_kernel_fn(const DevParams &p) {
     if (p.path != kPathSeg) return nullptr;
 #define GSM_PICK(n, no)                                                                  \
-    if (p.N == n && p.No == no && p.G == 1) {                                            \
+    if (p.N == n && p.No == no) {                                                        \
         switch (p.action_fmt) {                                                          \
             case 0: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 0>); \
             case 1: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 1>); \

@@ -756,6 +756,8 @@ __global__ __launch_bounds__(kTileBlock) void gsm_emit_tile_kernel(DevParams p) 
     int64_t off;   // (emit_env's exchange barrier also publishes the staged positions)
     emit_env(p, EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity}, s_pos, p.row_mask + eb * p.M * p.W, before,
              &off, s_red, s_scr, scr_cap, (int32_t)(eb * E));
+    // the emit launch that ends a rollout graph advances its granule epoch
+    if (p.roll.epoch && b == 0 && tid == 0) *p.roll.epoch = (*p.roll.epoch + 1u) & 0xffffu;
     if (tid == 0) {
         p.edge_ptr[b] = off;
         if (b == p.B - 1) p.edge_ptr[p.B] = off + p.edge_count[b];
@@ -839,6 +841,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     float2 acc = p.ep_acc[b];
     if (tid == 0) s_deg[0] = s_deg[1] = 0;
     const int K = p.roll.K, n_act = p.roll.n_actions;
+    const uint32_t etag = *p.roll.epoch << 16;              // this launch's tag base
     int arow = p.roll.t_first % n_act;
     int prev_edges = 0, bad = 0;
     __syncthreads();
@@ -996,7 +999,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             KernargParams &q = late_params();
             q.done[b] = done ? 1 : 0;
             __hip_atomic_store((gu64 *)(q.roll.gran + (int64_t)k * gridDim.x + b),
-                               ((uint64_t)(k + 1) << 32) | (uint32_t)edges, __ATOMIC_RELAXED,
+                               ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)edges, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
         // the previous step's edges at the offset of the look-back
@@ -1005,12 +1008,17 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             if (wave == 0) {
                 const int64_t kb = (int64_t)(k - 1) * gridDim.x;
                 KernargParams &q = late_params();
-                ex = roll_lookback(q.roll.gran + kb, q.roll.gran + (int64_t)K * gridDim.x + kb, (uint32_t)k,
+                ex = roll_lookback(q.roll.gran + kb, q.roll.gran + (int64_t)K * gridDim.x + kb, etag | (uint32_t)k,
                                    q.roll.status, lane);
                 if (lane == 0)
                     __hip_atomic_store((gu64 *)(late_params().roll.gran + (int64_t)K * gridDim.x + kb + b),
-                                       ((uint64_t)k << 32) | (uint32_t)(ex + prev_edges), __ATOMIC_RELAXED,
+                                       ((uint64_t)(etag | (uint32_t)k) << 32) | (uint32_t)(ex + prev_edges),
+                                       __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+            }
+            if (ex < 0 || ex > p.edge_capacity) {   // a broken hand-off: never write out of bounds
+                __hip_atomic_store((gu32 *)p.roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ex = (int)min(p.edge_capacity, (int64_t)0x7fffffff);
             }
             int64_t off;
             {

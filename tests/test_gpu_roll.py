@@ -55,6 +55,8 @@ def _same(ref, env, what):
 @pytest.mark.parametrize("N,B,T,EL,fmt", [(24, 64, 12, 5, "index"), (24, 257, 9, 7, "index"), (24, 8, 2, 5, "index"),
                                           (24, 40, 1, 5, "index"), (24, 130, 11, 5, "onehot"), (24, 99, 8, 3, "cont"),
                                           (24, 8192, 26, 25, "index"),
+                                          # C2's shape (the step kernels pack 4 envs per wave, the rollout one)
+                                          (3, 64, 12, 5, "index"), (3, 4096, 15, 6, "index"), (3, 4100, 7, 3, "onehot"),
                                           # tile path (one workgroup per env): C3's shape
                                           (96, 16, 9, 5, "index"), (96, 33, 6, 4, "onehot"), (96, 7, 5, 2, "cont"),
                                           (96, 1024, 12, 10, "index"), (70, 9, 3, 2, "index")])
@@ -88,7 +90,7 @@ def test_roll_equals_eager(N, B, T, EL, fmt):
     env.close()
 
 
-@pytest.mark.parametrize("N,B", [(24, 300), (96, 20)])
+@pytest.mark.parametrize("N,B", [(24, 300), (96, 20), (3, 4100)])
 def test_roll_emit_after_chain(N, B):
     """The bound edge-sum half holds the last step's sums after a rollout
     graph: an emit-only graph right after it re-emits the same edges."""
@@ -145,10 +147,34 @@ def test_roll_oracle_direct(N, B):
 
 
 def test_roll_rejected_where_unsupported():
+    """A runtime-shape segmented config (5 agents) has no rollout kernel."""
     from gsmarl_amd._lib import GsmError
-    env, cfg = _env(n_agents=3, n_envs=64)
-    acts = torch.randint(0, 5, (4, 64, 3), dtype=torch.int32, device=DEV)
+    env, cfg = _env(n_agents=5, n_envs=64)
+    acts = torch.randint(0, 5, (4, 64, 5), dtype=torch.int32, device=DEV)
     env.reset(seed=1)
     with pytest.raises(GsmError):
         env.capture(acts, 4, slot=0, kernels="roll")
+    env.close()
+
+
+@pytest.mark.parametrize("N,B", [(3, 4096), (24, 512), (96, 16)])
+def test_roll_replay_after_other_work(N, B):
+    """A rollout graph replayed after eager steps and a reset (the granules of
+    its previous replay are still in memory: the launch epoch in their tags
+    keeps them from being taken for this replay's) equals eager steps."""
+    T, EL = 15, 6
+    env, cfg = _env(n_agents=N, n_envs=B, episode_length=EL)
+    acts = torch.randint(0, 5, (T - 3, B, N), dtype=torch.int32, device=DEV)
+    env.reset(seed=11)
+    env.capture(acts, T, slot=0, kernels="roll")
+    env.replay(0)
+    for t in range(2 * T):
+        env.step(acts[t % acts.shape[0]], sync_edges=False)
+    ref = _eager(env, acts, 2 * T, seed=11)
+    env.reset(seed=11)
+    env.replay(0)
+    env.replay(0)
+    torch.cuda.synchronize()
+    assert not env.roll_gave_up()
+    _same(ref, env, "replay after eager work")
     env.close()
