@@ -170,7 +170,12 @@ def test_roll_replay_after_other_work(N, B):
     env.replay(0)
     for t in range(2 * T):
         env.step(acts[t % acts.shape[0]], sync_edges=False)
-    ref = _eager(env, acts, 2 * T, seed=11)
+    env.reset(seed=11)
+    for _ in range(2):   # two replays: each runs action rows j % len(acts), j < T
+        for t in range(T):
+            env.step(acts[t % acts.shape[0]], sync_edges=False)
+    torch.cuda.synchronize()
+    ref = {k: v.clone() for k, v in env.t.items()}
     env.reset(seed=11)
     env.replay(0)
     env.replay(0)
