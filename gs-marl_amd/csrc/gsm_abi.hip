@@ -39,7 +39,6 @@ struct gsm_handle {
         uint64_t *gran = nullptr;     // fused rollout: [K][n_blocks] edge-sum granules
     } slots[GSM_GRAPH_SLOTS];
     uint32_t *roll_status = nullptr;  // fused rollout: a bounded wait gave up (sticky until read)
-    uint64_t *roll_rows = nullptr;    // tile rollout: the second row-mask buffer [B][M][W]
 };
 
 namespace {
@@ -542,10 +541,6 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         e = hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking);
         if (e != hipSuccess) return hip_fail(h, e, "hipStreamCreate");
     }
-    if (tile && !h->roll_rows) {   // the tile rollout double-buffers the row masks
-        e = hipMalloc(&h->roll_rows, (size_t)p.B * p.M * p.W * sizeof(uint64_t));
-        if (e != hipSuccess) { h->roll_rows = nullptr; return hip_fail(h, e, "hipMalloc (rollout row masks)"); }
-    }
     const int K = n_steps;
     if (K > 65535) return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: n_steps must be <= 65535");
     // a 16-byte header (the launch epoch), then aggregates [K][nb] and
@@ -580,7 +575,7 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     p.lag = gsm::DevParams::Lag{p.block_edge_sum, p.edge_count, p.edge_ptr, p.edge_index, p.edge_attr,
                                 p.edge_capacity};
     p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, 0, sl.gran + 2, h->roll_status,
-                                  h->roll_rows, (uint32_t *)sl.gran};
+                                  (uint32_t *)sl.gran};
     if (e == hipSuccess) {
         what = "rollout kernel node";
         hipKernelNodeParams kp = {};
@@ -867,7 +862,6 @@ int gsm_destroy(gsm_handle *h) {
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->bsum_alt) (void)hipFree(h->bsum_alt);
     if (h->roll_status) (void)hipFree(h->roll_status);
-    if (h->roll_rows) (void)hipFree(h->roll_rows);
     if (h->order_copied) (void)hipEventSynchronize(h->order_copied);
     if (h->block_order) (void)hipFree(h->block_order);
     if (h->order_host) (void)hipHostFree(h->order_host);

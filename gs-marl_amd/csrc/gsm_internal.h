@@ -102,7 +102,6 @@ struct DevParams {
         int32_t n_actions, t_first, K, pad;
         uint64_t *gran;
         uint32_t *status;
-        uint64_t *rows_alt;   // tile path: [B][M][W] row masks of every other step (double buffer)
         uint32_t *epoch;      // nullptr outside rollout graphs (the emit kernel then leaves it)
     } roll;
 };

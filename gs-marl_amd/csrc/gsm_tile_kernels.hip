@@ -193,10 +193,11 @@ __device__ __forceinline__ uint64_t agent_bits_of_word(int N, int k) {   // agen
 
 // rout: where the row masks go; rkeep: where the cached obstacle-obstacle
 // words are read (keep_oo) — the same buffer except in the fused rollout,
-// which double-buffers the masks (the previous step's are emitted later)
+// which double-buffers the masks in LDS (the previous step's are emitted
+// later); cout: where the contact words go (LDS in the rollout)
 __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s_pos, const TileSymLds &S,
                                              int *s_cost, int64_t eb, bool keep_oo, uint64_t *rout = nullptr,
-                                             const uint64_t *rkeep = nullptr) {
+                                             const uint64_t *rkeep = nullptr, uint64_t *cout = nullptr) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     const int N = p.N, M = p.M, W = p.W, No = p.No;
     const int tid = threadIdx.x, lane = tid & 63;
@@ -256,7 +257,7 @@ __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s
     uint64_t *const rmask = rout ? rout : p.row_mask + eb * M * W;
     const uint64_t *const rprev = rkeep ? rkeep : rmask;
     const bool rewrite = rprev != rmask;                    // every word is written
-    uint64_t *const cmask = p.contact_mask + eb * N * W;
+    uint64_t *const cmask = cout ? cout : p.contact_mask + eb * N * W;
     int pairs = 0, coinc = 0;
     for (int r = tid; r < M; r += kTileBlock) {
         const float2 a = s_pos[collider_entity(r, N)];
@@ -767,20 +768,20 @@ __global__ __launch_bounds__(kTileBlock) void gsm_emit_tile_kernel(DevParams p) 
 // ---------------------------------------------------------------------------
 // Fused rollout on the tile path (one 512-thread workgroup per env; C3):
 // K steps of a graph in one launch, as gsm_roll_seg_kernel.
-// Positions and velocities stay in LDS; contact masks are re-read from global
-// memory written by this workgroup's previous sweep (a workgroup barrier
-// orders them); the row masks alternate between the bound buffer and
-// p.roll.rows_alt (step k writes slot (K-1-k) & 1, so the last step's masks
-// land in the bound buffer for the emit launch that follows), so step k-1's
-// masks survive step k's sweep and are emitted after it at the offset found
-// by the look-back over per-env granules (one env per workgroup). The step's
+// Positions, velocities, contact words and row masks stay in LDS; the row
+// masks alternate between two LDS buffers (step k writes k & 1) so step
+// k-1's masks survive step k's sweep and are emitted after it at the offset
+// found by the look-back over per-env granules (one env per workgroup); the
+// masks go to global memory once, after the loop (the emit launch that
+// follows reads the last step's). The step's
 // outputs (node features, reward, cost, done) are written every step, the
 // state once after the loop. Same operations as gsm_step_tile_kernel in the
 // same order: bit-identical outputs.
 constexpr int kRollTileScr = 2048;   // staged edge words (C3: ~390 edges per env; else direct writes)
 
 size_t roll_tile_kernel_lds(const DevParams &p) {
-    return (size_t)p.wave_lds_step + 8 * (size_t)p.E + 16 + 8 * kTileWaves + 4 * kRollTileScr;
+    return (size_t)p.wave_lds_step + 8 * (size_t)p.E + 16 + 8 * kTileWaves + 4 * kRollTileScr +
+           8 * (size_t)p.W * (2 * p.M + p.N);
 }
 
 template <typename Params>
@@ -830,9 +831,12 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     int *s_x = (int *)(s_prev + E);                        // [4]
     int *s_red = s_x + 4;                                  // [2 * kTileWaves] emit_env exchange
     uint32_t *s_scr = (uint32_t *)(s_red + 2 * kTileWaves);
+    uint64_t *s_rm = (uint64_t *)(s_scr + kRollTileScr);   // [2][M][W] row masks, step k at k & 1
+    uint64_t *s_cm = s_rm + 2 * M * W;                     // [N][W] contact words
     const int64_t eb = b;
     const int32_t g0 = (int32_t)(eb * E);
-    uint64_t *const rbuf[2] = {p.row_mask + eb * M * W, p.roll.rows_alt + eb * M * W};
+    for (int w = tid; w < M * W; w += kTileBlock) s_rm[M * W + w] = p.row_mask[eb * M * W + w];
+    for (int w = tid; w < N * W; w += kTileBlock) s_cm[w] = p.contact_mask[eb * N * W + w];
 
     for (int e = tid; e < E; e += kTileBlock) s_pos[e] = p.pos[eb * E + e];
     for (int i = tid; i < N; i += kTileBlock) s_vel[i] = p.vel[eb * N + i];
@@ -847,8 +851,13 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     __syncthreads();
 
     for (int k = 0; k < K; ++k) {
-        uint64_t *const rout = rbuf[(K - 1 - k) & 1];
-        const uint64_t *const rkeep = k == 0 ? rbuf[0] : rbuf[(K - k) & 1];   // the previous step's masks
+        // thread-derived values re-formed every iteration (an asm barrier): held
+        // across the loop their hoisted addresses would pin VGPRs
+        int tid = (int)threadIdx.x;
+        asm volatile("" : "+v"(tid));
+        const int wave = tid >> 6, lane = tid & 63;
+        uint64_t *const rout = s_rm + (k & 1) * M * W;
+        const uint64_t *const rkeep = s_rm + ((k + 1) & 1) * M * W;   // the previous step's masks
         bool relaid = false;
         auto relayout = [&]() {   // scenario.reset_world with the Philox layout
             ep = ep + 1;
@@ -862,7 +871,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             __syncthreads();
         };
         // apply_environment_force + integrate_state (as gsm_step_tile_kernel)
-        const uint64_t *cm = late_params().contact_mask + eb * N * W;
+        const uint64_t *cm = s_cm;
         for (int i = tid; i < N; i += kTileBlock) {
             const float2 pi = s_pos[i];
             const float2 u = roll_tile_force(late_params(), arow, eb * N + i);
@@ -907,7 +916,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         t += 1;
         const bool done = t >= p.EL;
 
-        int pairs = obs_sweep_sym(p, s_pos, sym, s_cost, eb, true, rout, rkeep);
+        int pairs = obs_sweep_sym(p, s_pos, sym, s_cost, eb, true, rout, rkeep, s_cm);
         auto nonfinite_part = [&]() {
             int bd = 0;
             if (p.degenerate)
@@ -963,7 +972,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         if (done && p.auto_reset) {
             if (tid == 0) late_params().ep_last[b] = acc;
             relayout();
-            pairs = obs_sweep_sym(p, s_pos, sym, s_cost, eb, false, rout, rkeep);
+            pairs = obs_sweep_sym(p, s_pos, sym, s_cost, eb, false, rout, rkeep, s_cm);
             pairs = tile_sum(pairs, s_ired);
             bad = tile_sum(nonfinite_part(), s_ired + 3 * kTileWaves);
         }
@@ -1040,6 +1049,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     }
     // the final state (what the next launch or an eager step reads)
     for (int e = tid; e < E; e += kTileBlock) p.pos[eb * E + e] = s_pos[e];
+    for (int w = tid; w < M * W; w += kTileBlock) p.row_mask[eb * M * W + w] = s_rm[((K - 1) & 1) * M * W + w];
+    for (int w = tid; w < N * W; w += kTileBlock) p.contact_mask[eb * N * W + w] = s_cm[w];
     for (int i = tid; i < N; i += kTileBlock) p.vel[eb * N + i] = s_vel[i];
     if (tid == 0) {
         p.step_count[b] = t;
