@@ -36,7 +36,8 @@ struct gsm_handle {
         int steps = 0;
         int kern = 0;
         bool each = false;
-        uint64_t *gran = nullptr;     // fused rollout: [K][n_blocks] edge-sum granules
+        uint64_t *gran = nullptr;     // fused rollout: epoch word, then the edge-sum granules
+        bool roll = false;            // the graph is one rollout launch (+ the final emit)
     } slots[GSM_GRAPH_SLOTS];
     uint32_t *roll_status = nullptr;  // fused rollout: a bounded wait gave up (sticky until read)
 };
@@ -348,6 +349,7 @@ void drop_slot(gsm_handle::Slot &s) {
     for (hipEvent_t ev : s.events) (void)hipEventDestroy(ev);
     if (s.gran) (void)hipFree(s.gran);
     s.gran = nullptr;
+    s.roll = false;
     s.exec = nullptr;
     s.graph = nullptr;
     s.events.clear();
@@ -363,6 +365,24 @@ void drop_graph(gsm_handle *h) {
 bool bad_slot(int32_t slot) { return slot < 0 || slot >= GSM_GRAPH_SLOTS; }
 
 }  // namespace
+
+// A per-step output field of the slots: every slot redirected at a constant
+// stride (base, stride), or none (the bound buffer, stride 0).
+template <typename T>
+static bool slot_field(const gsm_outputs *o, int n, T *gsm_outputs::*f, T **base, int64_t *stride) {
+    T *const b0 = o[0].*f;
+    if (!b0) {
+        for (int j = 1; j < n; ++j)
+            if (o[j].*f) return false;
+        return true;
+    }
+    const int64_t st = n > 1 ? (int64_t)(o[1].*f - b0) : 0;
+    for (int j = 0; j < n; ++j)
+        if (o[j].*f != b0 + j * st) return false;
+    *base = b0;
+    *stride = st;
+    return true;
+}
 
 extern "C" {
 
@@ -483,7 +503,9 @@ int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream) {
 static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_t stride, int32_t n_actions,
                         int32_t n_steps, int action_fmt, int flags, const gsm_outputs *per_step);
 static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_t stride, int32_t n_actions,
-                        int32_t n_steps, int action_fmt, int flags);
+                        int32_t n_steps, int action_fmt, int flags, const gsm_outputs *per_step = nullptr,
+                        bool fallback = false);
+constexpr int kRollIneligible = 1;   // capture_roll(fallback = true): use the per-step chain instead
 
 int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t stride,
                       int32_t n_actions, int32_t n_steps, int action_fmt, int flags) {
@@ -493,15 +515,21 @@ int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t 
 int gsm_graph_capture_into(gsm_handle *h, int32_t slot, const void *actions, int64_t stride,
                            int32_t n_actions, int32_t n_steps, int action_fmt, const gsm_outputs *per_step) {
     if (!per_step) return fail(h, GSM_EINVAL, "per_step outputs is NULL");
+    // one rollout launch when the config has a rollout kernel and the slots
+    // sit at constant strides (a rollout buffer), else the per-step chain
+    const int rc = capture_roll(h, slot, actions, stride, n_actions, n_steps, action_fmt, 0, per_step, true);
+    if (rc != kRollIneligible) return rc;
     return capture_impl(h, slot, actions, stride, n_actions, n_steps, action_fmt, 0, per_step);
 }
+
+
 
 // Fused rollout graph (GSM_GRAPH_ROLL): a zeroing memset of the granules, ONE
 // gsm_roll_seg_kernel launch for all n_steps steps (it emits the edges of all
 // but the last), the emit launch for the last step. Every output equals the
 // lagged chain's.
 static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_t stride, int32_t n_actions,
-                        int32_t n_steps, int action_fmt, int flags) {
+                        int32_t n_steps, int action_fmt, int flags, const gsm_outputs *per_step, bool fallback) {
     if (flags & ~(GSM_GRAPH_ROLL | GSM_GRAPH_TIME_ENDS))
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL combines with GSM_GRAPH_TIME_ENDS only");
     if (!actions || n_actions < 1 || stride < 0) return fail(h, GSM_EINVAL, "bad capture arguments");
@@ -514,9 +542,37 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     p.reseed = 0;
     const bool tile = p.path == gsm::kPathTile;
     const void *roll_fn = tile ? gsm::roll_tile_kernel_fn(p) : gsm::roll_seg_kernel_fn(p);
+    if (!roll_fn && fallback) return kRollIneligible;
     if (!roll_fn) return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: no fused rollout kernel for this config "
                                              "(segmented path with a compiled shape, or tile path with the "
                                              "symmetric sweep)");
+    // step k's outputs at base + k * stride (a rollout buffer's slots) or all
+    // in the bound buffers
+    gsm::DevParams::RollOut ro{p.node_feat, p.reward, p.cost, p.done, p.edge_count, p.edge_ptr, p.edge_index,
+                               p.edge_attr, 0, 0, 0, 0, 0, 0, 0, p.edge_capacity};
+    if (per_step) {
+        int64_t cost_s = 0;
+        bool ok = slot_field(per_step, n_steps, &gsm_outputs::node_feat, &ro.nf, &ro.nf_s) &&
+                  slot_field(per_step, n_steps, &gsm_outputs::reward, &ro.rew, &ro.rc_s) &&
+                  slot_field(per_step, n_steps, &gsm_outputs::cost, &ro.cost, &cost_s) &&
+                  slot_field(per_step, n_steps, &gsm_outputs::done, &ro.done, &ro.done_s) &&
+                  slot_field(per_step, n_steps, &gsm_outputs::edge_count, &ro.ecount, &ro.ec_s) &&
+                  slot_field(per_step, n_steps, &gsm_outputs::edge_ptr, &ro.eptr, &ro.ep_s) &&
+                  slot_field(per_step, n_steps, &gsm_outputs::edge_index, &ro.eidx, &ro.ei_s) &&
+                  slot_field(per_step, n_steps, &gsm_outputs::edge_attr, &ro.eattr, &ro.ea_s) &&
+                  cost_s == ro.rc_s && !per_step[0].assign;
+        for (int j = 0; ok && j < n_steps; ++j) {
+            const int rc = redirect(h, &p, &per_step[j]);   // validates the slot
+            if (rc) return rc;
+            ok = !per_step[0].edge_index || per_step[j].edge_capacity == per_step[0].edge_capacity;
+        }
+        if (!ok) {
+            if (fallback) return kRollIneligible;
+            return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: per-step outputs must sit at constant strides");
+        }
+        if (per_step[0].edge_index) ro.cap = per_step[0].edge_capacity;
+        // p now describes the last slot: the final emit launch writes it
+    }
     // segmented rollout: one env per wave whatever the config's G (4 per workgroup)
     const int nb = tile ? gsm::step_grid_blocks(p) : (p.B + gsm::kWavesPerBlock - 1) / gsm::kWavesPerBlock;
     const size_t roll_lds = tile ? gsm::roll_tile_kernel_lds(p) : gsm::roll_kernel_lds(p);
@@ -528,8 +584,10 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     if (e == hipSuccess)
         e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, roll_fn, gsm::block_threads(p), roll_lds);
     if (e != hipSuccess) return hip_fail(h, e, "occupancy query");
-    if ((int64_t)per_cu * n_cu < nb)
+    if ((int64_t)per_cu * n_cu < nb) {
+        if (fallback) return kRollIneligible;
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: the batch exceeds one residency round of the rollout kernel");
+    }
     gsm_handle::Slot &sl = h->slots[slot];
     drop_slot(sl);
     if (!h->roll_status) {
@@ -572,8 +630,7 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     // all steps in one launch; the last step's sums go to the bound edge-sum
     // buffer (later eager emits read it); edges go to the bound outputs
     p.actions = actions;
-    p.lag = gsm::DevParams::Lag{p.block_edge_sum, p.edge_count, p.edge_ptr, p.edge_index, p.edge_attr,
-                                p.edge_capacity};
+    p.ro = ro;
     p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, 0, sl.gran + 2, h->roll_status,
                                   (uint32_t *)sl.gran};
     if (e == hipSuccess) {
@@ -621,6 +678,16 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     sl.each = false;
     sl.kern = GSM_GRAPH_STEP;
     sl.steps = n_steps;
+    sl.roll = true;
+    return GSM_OK;
+}
+
+int gsm_graph_info(gsm_handle *h, int32_t slot, int32_t *steps, int32_t *fused) {
+    if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
+    if (bad_slot(slot)) return fail(h, GSM_EINVAL, "bad graph slot");
+    const gsm_handle::Slot &sl = h->slots[slot];
+    if (steps) *steps = sl.exec ? sl.steps : 0;
+    if (fused) *fused = sl.exec && sl.roll ? 1 : 0;
     return GSM_OK;
 }
 

@@ -104,6 +104,19 @@ struct DevParams {
         uint32_t *status;
         uint32_t *epoch;      // nullptr outside rollout graphs (the emit kernel then leaves it)
     } roll;
+    // A rollout's per-step outputs: step k's at base + k * stride (elements;
+    // stride 0 = every step into the bound buffers, > 0 = a rollout buffer's
+    // slots, gsm_graph_capture_into). Edges of step k at index / attr + k *
+    // e_s, edge_ptr + k * ep_s, capacity cap.
+    struct RollOut {
+        float *nf, *rew, *cost;
+        uint8_t *done;
+        int32_t *ecount;
+        int64_t *eptr;
+        int32_t *eidx;
+        float *eattr;
+        int64_t nf_s, rc_s, done_s, ec_s, ep_s, ei_s, ea_s, cap;
+    } ro;
 };
 
 // where an emission writes its edges

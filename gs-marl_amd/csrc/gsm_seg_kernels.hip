@@ -1286,8 +1286,8 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         const int csum = wave_total(ci);
         if (L.agent) {
             KernargParams &q = late_params();
-            (q.reward + eb * N)[um] = p.shared_reward ? rsum : r;
-            (q.cost + eb * N)[um] = (float)ci;
+            (q.ro.rew + k * q.ro.rc_s + eb * N)[um] = p.shared_reward ? rsum : r;
+            (q.ro.cost + k * q.ro.rc_s + eb * N)[um] = (float)ci;
         }
         if (p.shared_reward) rsum *= (float)N;
         if (L.live) {
@@ -1332,7 +1332,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         KernargParams &q = late_params();
         const bool any_statics = p.nf_full || __any(relaid);
         if (L.live) {
-            float *nf = q.node_feat + eb * E * 7;
+            float *nf = q.ro.nf + k * q.ro.nf_s + eb * E * 7;
             if (L.agent) {
                 const float2 g = s_pos[N + m];
                 store_row(nf + m * 7, v, pm, make_float2(g.x - pm.x, g.y - pm.y), 0.0f);
@@ -1348,7 +1348,10 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         }
         const int edges = __popcll(row) + ((L.live && m == 0) ? 2 * N : 0);
         const int wave_edges = wave_total(edges);
-        if (wave_live && L.lane == 0) q.done[L.b] = done ? 1 : 0;
+        if (wave_live && L.lane == 0) {
+            (q.ro.done + k * q.ro.done_s)[L.b] = done ? 1 : 0;
+            (q.ro.ecount + k * q.ro.ec_s)[L.b] = wave_edges;
+        }
 
         // publish the workgroup's edge sum of step t
         const int par = k & 1;
@@ -1415,17 +1418,20 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             for (int w = 0; w < kWavesPerBlock; ++w) before += w < wave ? cb[w] : 0;
             const int my_cnt = cb[wave];
             int64_t env_off = (int64_t)s_red[0] + before;
-            if (env_off < 0 || env_off > p.lag.cap) {   // a broken hand-off: never write out of bounds
+            // (an offset past the capacity is a legal overflow of a small slot:
+            // edge_ptr keeps it, the writes below stop at the capacity)
+            if (env_off < 0) {   // a broken hand-off: never write out of bounds
                 if (L.lane == 0) __hip_atomic_store((gu32 *)p.roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                env_off = p.lag.cap;
+                env_off = p.ro.cap;
             }
             if (wave_live) {
                 KernargParams &qs = late_params();
                 if (L.lane == 0) {
-                    qs.lag.edge_ptr[L.b] = env_off;
-                    if (L.b == p.B - 1) qs.lag.edge_ptr[p.B] = env_off + my_cnt;
+                    int64_t *const eptr = qs.ro.eptr + (k - 1) * qs.ro.ep_s;
+                    eptr[L.b] = env_off;
+                    if (L.b == p.B - 1) eptr[p.B] = env_off + my_cnt;
                 }
-                const EdgeSink out{qs.lag.edge_index, qs.lag.edge_attr, qs.lag.cap};
+                const EdgeSink out{qs.ro.eidx + (k - 1) * qs.ro.ei_s, qs.ro.eattr + (k - 1) * qs.ro.ea_s, qs.ro.cap};
                 if (staged >= 0 && env_off + staged <= out.cap)
                     write_staged<kN, kNo>(L, s_prev, (uint32_t *)s_nf, staged, env_off, out);
                 else
@@ -1460,7 +1466,6 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             q.step_count[L0.b] = t;
             q.episode[L0.b] = ep;
             q.ep_acc[L0.b] = acc;
-            q.edge_count[L0.b] = s_bc[((K - 1) & 1) * kWavesPerBlock + wave];
             if (q.degenerate) q.degenerate[L0.b] = deg;
         }
     }

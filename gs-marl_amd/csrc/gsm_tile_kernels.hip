@@ -933,12 +933,12 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         int cpart = 0;
         for (int i = tid; i < N; i += kTileBlock) {
             const int cnt = s_cost[i];
-            late_params().cost[eb * N + i] = (float)cnt;
+            late_params().ro.cost[k * p.ro.rc_s + eb * N + i] = (float)cnt;
             cpart += cnt;
             if (!p.shared_reward) {
                 const float2 a = s_pos[i], g = s_pos[N + i];
                 const float dx = a.x - g.x, dy = a.y - g.y;
-                late_params().reward[eb * N + i] = -sqrtf(dx * dx + dy * dy);
+                late_params().ro.rew[k * p.ro.rc_s + eb * N + i] = -sqrtf(dx * dx + dy * dy);
             }
         }
         {
@@ -964,7 +964,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             bad |= s_ired[2 * kTileWaves + w];
         }
         if (p.shared_reward) {
-            for (int i = tid; i < N; i += kTileBlock) late_params().reward[eb * N + i] = rsum;
+            for (int i = tid; i < N; i += kTileBlock) late_params().ro.rew[k * p.ro.rc_s + eb * N + i] = rsum;
             rsum *= (float)N;
         }
         acc.x += rsum;
@@ -977,7 +977,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             bad = tile_sum(nonfinite_part(), s_ired + 3 * kTileWaves);
         }
         // the step's observation outputs: agent node rows, static rows on a new layout
-        float *nf = late_params().node_feat + eb * E * 7;
+        float *nf = late_params().ro.nf + k * p.ro.nf_s + eb * E * 7;
         const bool full = relaid || p.nf_full;
         for (int i = tid; i < N; i += kTileBlock) {
             const float2 v = s_vel[i], a = s_pos[i], g = s_pos[N + i];
@@ -1006,7 +1006,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         const int edges = pairs + 2 * N;   // directed radius edges + agent<->goal
         if (tid == 0) {
             KernargParams &q = late_params();
-            q.done[b] = done ? 1 : 0;
+            q.ro.done[k * q.ro.done_s + b] = done ? 1 : 0;
+            q.ro.ecount[k * q.ro.ec_s + b] = edges;
             __hip_atomic_store((gu64 *)(q.roll.gran + (int64_t)k * gridDim.x + b),
                                ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)edges, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -1025,20 +1026,24 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                                        __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
-            if (ex < 0 || ex > p.edge_capacity) {   // a broken hand-off: never write out of bounds
+            // (an offset past the capacity is a legal overflow of a small slot:
+            // edge_ptr keeps it, emit_env stops its writes at the capacity)
+            if (ex < 0) {   // a broken hand-off: never write out of bounds
                 __hip_atomic_store((gu32 *)p.roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ex = (int)min(p.edge_capacity, (int64_t)0x7fffffff);
+                ex = (int)min(p.ro.cap, (int64_t)0x7fffffff);
             }
             int64_t off;
             {
                 KernargParams &q = late_params();
-                emit_env(p, EdgeSink{q.edge_index, q.edge_attr, q.edge_capacity}, s_prev, rkeep, tid == 0 ? ex : 0,
+                emit_env(p, EdgeSink{q.ro.eidx + (k - 1) * q.ro.ei_s, q.ro.eattr + (k - 1) * q.ro.ea_s, q.ro.cap},
+                         s_prev, rkeep, tid == 0 ? ex : 0,
                          &off, s_red, s_scr, kRollTileScr, g0);
             }
             if (tid == 0) {
                 KernargParams &q = late_params();
-                q.edge_ptr[b] = off;
-                if (b == p.B - 1) q.edge_ptr[p.B] = off + prev_edges;
+                int64_t *const eptr = q.ro.eptr + (k - 1) * q.ro.ep_s;
+                eptr[b] = off;
+                if (b == p.B - 1) eptr[p.B] = off + prev_edges;
             }
         }
         __syncthreads();   // s_prev and the staged words read
@@ -1056,7 +1061,6 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         p.step_count[b] = t;
         p.episode[b] = ep;
         p.ep_acc[b] = acc;
-        p.edge_count[b] = prev_edges;
         p.block_edge_sum[b] = prev_edges;
         if (p.degenerate) p.degenerate[b] = (uint8_t)((*sym.flag ? kDegCoincident : 0) | (bad ? kDegNonfinite : 0));
     }

@@ -82,6 +82,7 @@ SIGNATURES = {
     "gsm_graph_capture": (C.c_int, [_P, C.c_int32, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int, C.c_int]),
     "gsm_graph_launch": (C.c_int, [_P, C.c_int32, _P]),
     "gsm_graph_roll_status": (C.c_int, [_P, C.POINTER(C.c_int32)]),
+    "gsm_graph_info": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_int32), C.POINTER(C.c_int32)]),
     "gsm_graph_kernel_ms": (C.c_int, [_P, C.c_int32, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                       C.POINTER(C.c_float)]),
     "gsm_attn_aggregate": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, C.c_int64, C.c_int32, C.c_int32, C.c_float,

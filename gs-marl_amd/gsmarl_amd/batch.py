@@ -299,6 +299,13 @@ class GpuBatchEnv:
     def replay(self, slot: int = 0) -> None:
         self._chk(self.lib.gsm_graph_launch(self._h, int(slot), self._stream()), "gsm_graph_launch")
 
+    def graph_is_rollout(self, slot: int = 0) -> bool:
+        """Whether graph ``slot`` is one fused rollout launch (GSM_GRAPH_ROLL,
+        or capture_into on a rollout buffer) rather than a per-step chain."""
+        steps, fused = C.c_int32(), C.c_int32()
+        self._chk(self.lib.gsm_graph_info(self._h, int(slot), C.byref(steps), C.byref(fused)), "gsm_graph_info")
+        return bool(fused.value)
+
     def roll_gave_up(self) -> bool:
         """Whether a bounded wait of a fused rollout launch timed out since
         the last call (outputs of that launch invalid); clears the flag."""

@@ -35,7 +35,7 @@ extern "C" {
 /* 4: lagged-emission graph chains (GSM_GRAPH_UNFUSED / _LAG_ONLY), gsm_render
  * 5: degenerate-state handling: gsm_config.strict_degenerate,
  *    gsm_buffers.degenerate */
-/* 6: fused rollout graphs (GSM_GRAPH_ROLL, gsm_graph_roll_status) */
+/* 6: fused rollout graphs (GSM_GRAPH_ROLL, gsm_graph_roll_status, gsm_graph_info) */
 #define GSM_ABI_VERSION 6
 
 typedef enum gsm_status {
@@ -253,10 +253,17 @@ int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream);
 int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t action_stride_bytes,
                       int32_t n_actions, int32_t n_steps, int action_fmt, int flags);
 /* As gsm_graph_capture (both kernels, no timing events), with the j-th
- * step's outputs redirected to per_step[j] (n_steps entries). */
+ * step's outputs redirected to per_step[j] (n_steps entries). Where the config
+ * has a rollout kernel (GSM_GRAPH_ROLL) and every redirected field of the
+ * slots sits at a constant stride (a rollout buffer), the graph is one rollout
+ * launch writing step j's outputs into slot j; else the per-step chain. */
 int gsm_graph_capture_into(gsm_handle *h, int32_t slot, const void *actions, int64_t action_stride_bytes,
                            int32_t n_actions, int32_t n_steps, int action_fmt, const gsm_outputs *per_step);
 int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream);
+/* The graph in `slot`: its step count (0 if none) and whether it is one
+ * fused rollout launch (GSM_GRAPH_ROLL, or gsm_graph_capture_into on a
+ * rollout buffer) rather than a per-step chain. */
+int gsm_graph_info(gsm_handle *h, int32_t slot, int32_t *steps, int32_t *fused);
 /* After GSM_GRAPH_ROLL launches have completed: *gave_up = 1 if any bounded
  * wait of a rollout launch timed out since the last call (its outputs are
  * then invalid), else 0. Clears the flag. */

@@ -65,7 +65,11 @@ def test_graph_rollout_matches_eager(N, B, T):
     eb = GraphRolloutBuffer(ref, episode_length=T)
     gb.reset(seed=2)
     gb.capture(acts)
+    # compiled segmented shapes and tile shapes run the episode as one fused
+    # rollout launch writing slot j at base + j * stride
+    assert env.graph_is_rollout(0) == (N in (3, 24, 80))
     gb.replay()
+    assert not env.roll_gave_up()
     eb.reset(seed=2)
     for t in range(T):
         eb.insert(acts[t])
@@ -104,7 +108,7 @@ def test_edge_overflow_is_truncated():
 
 @pytest.mark.parametrize("N,B", [(24, 32), (3, 50)])
 def test_graph_chain_overflow_is_truncated(N, B):
-    """A lagged graph chain into slots far too small: every slot keeps its
+    """A rollout graph into slots far too small: every slot keeps its
     true CSR offsets and exactly the prefix of edges that fits; no slot's
     emission spills into another slot (each is checked against a plain env)."""
     from gsmarl_amd import GraphRolloutBuffer
@@ -114,7 +118,9 @@ def test_graph_chain_overflow_is_truncated(N, B):
     buf = GraphRolloutBuffer(env, episode_length=T, edges_per_env=2)
     buf.reset(seed=6)
     buf.capture(acts)
+    assert env.graph_is_rollout(0)   # the rollout launch truncates exactly as the chain does
     buf.replay()
+    assert not env.roll_gave_up()
     outs = [ref.reset(seed=6)]
     outs[0] = {k: v.clone() for k, v in outs[0].items()}
     for t in range(T):
