@@ -33,6 +33,8 @@ def main():
     ap.add_argument("--T", type=int, default=100)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--sweep", action="store_true", help="whole-graph time vs graph length (fixed cost)")
+    ap.add_argument("--buffer", action="store_true",
+                    help="also an episode into a GraphRolloutBuffer (per-step slots) via capture_into")
     a = ap.parse_args()
     env = GpuBatchEnv(EnvConfig(n_agents=a.N, n_envs=a.B, seed=1234), "cuda:0")
     acts = torch.randint(0, 5, (100, a.B, a.N), dtype=torch.int32, device="cuda:0")
@@ -51,6 +53,14 @@ def main():
     env.replay(1)
     torch.cuda.synchronize()
     out["roll_kernel_us_per_step"] = round(env.graph_kernel_ms(1)[0] * 1e3, 3)
+    if a.buffer:   # every step's outputs into its own slot (distinct addresses)
+        from gsmarl_amd import GraphRolloutBuffer
+        buf = GraphRolloutBuffer(env, episode_length=a.T)
+        buf.reset(seed=1234)
+        buf.capture(acts[: a.T], slot=2)
+        out["buffer_fused"] = env.graph_is_rollout(2)
+        out["buffer_graph_us_per_step"] = round(timed(env, 2, a.reps) * 1e3 / a.T, 3)
+        out["buffer_overflowed"] = bool(buf.overflowed())
     out["gave_up"] = env.roll_gave_up()
     print(json.dumps(out), flush=True)
     env.close()
