@@ -113,6 +113,17 @@ def roll_step_bytes(B, N, No, EL, action_bytes, total_edges, seg=True):
     return B * (action_bytes * N + writes + reset) + 12 * total_edges
 
 
+def survey_bytes_per_agent_step(N, No, action_bytes, total_edges, B):
+    """SURVEY.md §8(d)'s algorithmic bytes per agent-step, the per-unit figure
+    the contract prices a whole step at: B_as = 32 (pos+vel read+write) + A
+    (action) + 8 (own goal) + 8·No/N (obstacle positions) + 9 (reward, cost,
+    done) + (E/N)·F·4 (node table, F = 7) + 12·ē (edges per agent: int32 src,
+    dst + fp32 distance), ē measured."""
+    E = 2 * N + No
+    ebar = total_edges / (B * N)
+    return 32 + action_bytes + 8 + 8 * No / N + 9 + (E / N) * 7 * 4 + 12 * ebar
+
+
 def ragged_kernel_bytes(env, EL, action_bytes, total_edges):
     """Algorithmic HBM bytes of one ragged step / emit launch, summed over the
     batch's actual env shapes (N_env agents, T targets, M colliders).
@@ -618,6 +629,15 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False):
         eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)
         fam = "seg" if seg else "tile"
         names = (f"gsm_step_{fam}_kernel" + ("<lagged emission>" if lag else ""), f"gsm_emit_{fam}_kernel")
+    # a launch that runs whole steps (a rollout step, a lagged step kernel:
+    # physics, observation and the edges) is priced at SURVEY.md §8(d)'s
+    # per-unit figure x the agents it steps — the contract's algorithmic bytes;
+    # the kernel's own count of what it must move stays beside it
+    kernel_bytes = sb
+    bytes_model = "kernel count (bench.py step/emit/ragged_kernel_bytes)"
+    if (roll or lag) and not cfg.ragged:
+        sb = survey_bytes_per_agent_step(N, cfg.n_obstacles, 4, edges_now, B) * B * N
+        bytes_model = "SURVEY.md §8(d) B_as per agent-step x agents per step"
     kern = {"step": dict(kernel=names[0], ms=step_ms, bytes=sb, gbs=sb / (step_ms * 1e-3) / 1e9),
             "emit": dict(kernel=names[1], ms=emit_ms, bytes=eb, gbs=eb / (emit_ms * 1e-3) / 1e9)}
     # a lagged chain / rollout runs the emit kernel once per graph, the step kernel every step
@@ -649,7 +669,10 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False):
                     traffic=round(pmc["hbm_bytes_per_launch"]) if pmc else None,
                     pmc=dict(key=pkey, status=note, valu=valu,
                              source=pmc.get("source") if pmc else None),
-                    algorithmic_bytes_per_launch=int(k["bytes"]), mean_launch_us=round(k["ms"] * 1e3, 3),
+                    algorithmic_bytes_per_launch=int(k["bytes"]),
+                    bytes_model=bytes_model if dom == "step" else "kernel count",
+                    kernel_bytes_per_launch=int(kernel_bytes) if dom == "step" else int(k["bytes"]),
+                    mean_launch_us=round(k["ms"] * 1e3, 3),
                     timing=(f"HIP events around one fused rollout launch of {L} steps (time per step)" if roll
                             else f"HIP events around {L} back-to-back graph launches of the kernel"),
                     other_kernel=dict(kernel=other["kernel"], achieved=round(other["gbs"], 1),
