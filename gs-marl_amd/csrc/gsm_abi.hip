@@ -541,7 +541,8 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     p.env_mask = nullptr;
     p.reseed = 0;
     const bool tile = p.path == gsm::kPathTile;
-    const void *roll_fn = tile ? gsm::roll_tile_kernel_fn(p) : gsm::roll_seg_kernel_fn(p);
+    const bool slots = per_step != nullptr;
+    const void *roll_fn = tile ? gsm::roll_tile_kernel_fn(p, slots) : gsm::roll_seg_kernel_fn(p, slots);
     if (!roll_fn && fallback) return kRollIneligible;
     if (!roll_fn) return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: no fused rollout kernel for this config "
                                              "(segmented path with a compiled shape, or tile path with the "

@@ -143,9 +143,9 @@ const void *lag_step_seg_kernel_fn(const DevParams &p);
 const void *emit_seg_kernel_fn(const DevParams &p);
 // fused K-step rollout kernel (nullptr where the config has none: G > 1,
 // runtime shapes, other families) and its LDS bytes
-const void *roll_seg_kernel_fn(const DevParams &p);
+const void *roll_seg_kernel_fn(const DevParams &p, bool slots);   // slots: a rollout buffer's outputs
 size_t roll_kernel_lds(const DevParams &p);
-const void *roll_tile_kernel_fn(const DevParams &p);   // nullptr unless p.tile_sym
+const void *roll_tile_kernel_fn(const DevParams &p, bool slots);   // nullptr unless p.tile_sym
 size_t roll_tile_kernel_lds(const DevParams &p);
 const void *step_ragged_kernel_fn();
 const void *step_tile_kernel_fn();

@@ -1167,7 +1167,9 @@ __device__ __forceinline__ float2 roll_force(const Params &p, float4 a, bool age
     return agent ? make_float2(ux * p.sens, uy * p.sens) : make_float2(0.0f, 0.0f);
 }
 
-template <int kN, int kNo, int kFmt>
+// kSlots: per-step outputs at base + k * stride (a rollout buffer); else every
+// step into the bound buffers (the strides are 0 and fold away)
+template <int kN, int kNo, int kFmt, bool kSlots>
 __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevParams p) {
     static_assert(kN > 0 && kN <= 31 && kNo <= 32 && kFmt >= 0, "compile-time shape, staged emission");
     constexpr int N = kN, M = kN + kNo, E = 2 * kN + kNo;
@@ -1286,8 +1288,8 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         const int csum = wave_total(ci);
         if (L.agent) {
             KernargParams &q = late_params();
-            (q.ro.rew + k * q.ro.rc_s + eb * N)[um] = p.shared_reward ? rsum : r;
-            (q.ro.cost + k * q.ro.rc_s + eb * N)[um] = (float)ci;
+            (q.ro.rew + (kSlots ? k * q.ro.rc_s : 0) + eb * N)[um] = p.shared_reward ? rsum : r;
+            (q.ro.cost + (kSlots ? k * q.ro.rc_s : 0) + eb * N)[um] = (float)ci;
         }
         if (p.shared_reward) rsum *= (float)N;
         if (L.live) {
@@ -1332,7 +1334,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         KernargParams &q = late_params();
         const bool any_statics = p.nf_full || __any(relaid);
         if (L.live) {
-            float *nf = q.ro.nf + k * q.ro.nf_s + eb * E * 7;
+            float *nf = q.ro.nf + (kSlots ? k * q.ro.nf_s : 0) + eb * E * 7;
             if (L.agent) {
                 const float2 g = s_pos[N + m];
                 store_row(nf + m * 7, v, pm, make_float2(g.x - pm.x, g.y - pm.y), 0.0f);
@@ -1349,8 +1351,8 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         const int edges = __popcll(row) + ((L.live && m == 0) ? 2 * N : 0);
         const int wave_edges = wave_total(edges);
         if (wave_live && L.lane == 0) {
-            (q.ro.done + k * q.ro.done_s)[L.b] = done ? 1 : 0;
-            (q.ro.ecount + k * q.ro.ec_s)[L.b] = wave_edges;
+            (q.ro.done + (kSlots ? k * q.ro.done_s : 0))[L.b] = done ? 1 : 0;
+            if (kSlots || k == K - 1) (q.ro.ecount + (kSlots ? k * q.ro.ec_s : 0))[L.b] = wave_edges;
         }
 
         // publish the workgroup's edge sum of step t
@@ -1427,11 +1429,12 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             if (wave_live) {
                 KernargParams &qs = late_params();
                 if (L.lane == 0) {
-                    int64_t *const eptr = qs.ro.eptr + (k - 1) * qs.ro.ep_s;
+                    int64_t *const eptr = qs.ro.eptr + (kSlots ? (k - 1) * qs.ro.ep_s : 0);
                     eptr[L.b] = env_off;
                     if (L.b == p.B - 1) eptr[p.B] = env_off + my_cnt;
                 }
-                const EdgeSink out{qs.ro.eidx + (k - 1) * qs.ro.ei_s, qs.ro.eattr + (k - 1) * qs.ro.ea_s, qs.ro.cap};
+                const EdgeSink out{qs.ro.eidx + (kSlots ? (k - 1) * qs.ro.ei_s : 0),
+                                   qs.ro.eattr + (kSlots ? (k - 1) * qs.ro.ea_s : 0), qs.ro.cap};
                 if (staged >= 0 && env_off + staged <= out.cap)
                     write_staged<kN, kNo>(L, s_prev, (uint32_t *)s_nf, staged, env_off, out);
                 else
@@ -1494,19 +1497,23 @@ static const void *pick_step_seg(const DevParams &p) {
 const void *step_seg_kernel_fn(const DevParams &p) { return pick_step_seg<false>(p); }
 const void *lag_step_seg_kernel_fn(const DevParams &p) { return pick_step_seg<true>(p); }
 
-const void *roll_seg_kernel_fn(const DevParams &p) {
-    if (p.path != kPathSeg) return nullptr;
-#define GSM_PICK(n, no)                                                                  \
-    if (p.N == n && p.No == no) {                                                        \
-        switch (p.action_fmt) {                                                          \
-            case 0: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 0>); \
-            case 1: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 1>); \
-            default: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 2>); \
-        }                                                                                \
+template <bool kSlots>
+static const void *pick_roll_seg(const DevParams &p) {
+#define GSM_PICK(n, no)                                                                          \
+    if (p.N == n && p.No == no) {                                                                \
+        switch (p.action_fmt) {                                                                  \
+            case 0: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 0, kSlots>); \
+            case 1: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 1, kSlots>); \
+            default: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 2, kSlots>); \
+        }                                                                                        \
     }
     GSM_ROLL_SHAPES(GSM_PICK)
 #undef GSM_PICK
     return nullptr;
+}
+const void *roll_seg_kernel_fn(const DevParams &p, bool slots) {
+    if (p.path != kPathSeg) return nullptr;
+    return slots ? pick_roll_seg<true>(p) : pick_roll_seg<false>(p);
 }
 size_t roll_kernel_lds(const DevParams &p) {
     return (size_t)kWavesPerBlock * (p.wave_lds_step + 8 * p.E) + 64;

@@ -804,6 +804,7 @@ __device__ __forceinline__ float2 roll_tile_force(const Params &p, int row, int6
     return make_float2(ux * p.sens, uy * p.sens);
 }
 
+template <bool kSlots>   // per-step outputs at base + k * stride (a rollout buffer), else in place
 __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int b = blockIdx.x;
@@ -933,12 +934,12 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         int cpart = 0;
         for (int i = tid; i < N; i += kTileBlock) {
             const int cnt = s_cost[i];
-            late_params().ro.cost[k * p.ro.rc_s + eb * N + i] = (float)cnt;
+            late_params().ro.cost[(kSlots ? k * p.ro.rc_s : 0) + eb * N + i] = (float)cnt;
             cpart += cnt;
             if (!p.shared_reward) {
                 const float2 a = s_pos[i], g = s_pos[N + i];
                 const float dx = a.x - g.x, dy = a.y - g.y;
-                late_params().ro.rew[k * p.ro.rc_s + eb * N + i] = -sqrtf(dx * dx + dy * dy);
+                late_params().ro.rew[(kSlots ? k * p.ro.rc_s : 0) + eb * N + i] = -sqrtf(dx * dx + dy * dy);
             }
         }
         {
@@ -964,7 +965,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             bad |= s_ired[2 * kTileWaves + w];
         }
         if (p.shared_reward) {
-            for (int i = tid; i < N; i += kTileBlock) late_params().ro.rew[k * p.ro.rc_s + eb * N + i] = rsum;
+            for (int i = tid; i < N; i += kTileBlock) late_params().ro.rew[(kSlots ? k * p.ro.rc_s : 0) + eb * N + i] = rsum;
             rsum *= (float)N;
         }
         acc.x += rsum;
@@ -977,7 +978,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             bad = tile_sum(nonfinite_part(), s_ired + 3 * kTileWaves);
         }
         // the step's observation outputs: agent node rows, static rows on a new layout
-        float *nf = late_params().ro.nf + k * p.ro.nf_s + eb * E * 7;
+        float *nf = late_params().ro.nf + (kSlots ? k * p.ro.nf_s : 0) + eb * E * 7;
         const bool full = relaid || p.nf_full;
         for (int i = tid; i < N; i += kTileBlock) {
             const float2 v = s_vel[i], a = s_pos[i], g = s_pos[N + i];
@@ -1006,8 +1007,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         const int edges = pairs + 2 * N;   // directed radius edges + agent<->goal
         if (tid == 0) {
             KernargParams &q = late_params();
-            q.ro.done[k * q.ro.done_s + b] = done ? 1 : 0;
-            q.ro.ecount[k * q.ro.ec_s + b] = edges;
+            q.ro.done[(kSlots ? k * q.ro.done_s : 0) + b] = done ? 1 : 0;
+            if (kSlots || k == K - 1) q.ro.ecount[(kSlots ? k * q.ro.ec_s : 0) + b] = edges;
             __hip_atomic_store((gu64 *)(q.roll.gran + (int64_t)k * gridDim.x + b),
                                ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)edges, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -1035,13 +1036,14 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             int64_t off;
             {
                 KernargParams &q = late_params();
-                emit_env(p, EdgeSink{q.ro.eidx + (k - 1) * q.ro.ei_s, q.ro.eattr + (k - 1) * q.ro.ea_s, q.ro.cap},
+                emit_env(p, EdgeSink{q.ro.eidx + (kSlots ? (k - 1) * q.ro.ei_s : 0),
+                                     q.ro.eattr + (kSlots ? (k - 1) * q.ro.ea_s : 0), q.ro.cap},
                          s_prev, rkeep, tid == 0 ? ex : 0,
                          &off, s_red, s_scr, kRollTileScr, g0);
             }
             if (tid == 0) {
                 KernargParams &q = late_params();
-                int64_t *const eptr = q.ro.eptr + (k - 1) * q.ro.ep_s;
+                int64_t *const eptr = q.ro.eptr + (kSlots ? (k - 1) * q.ro.ep_s : 0);
                 eptr[b] = off;
                 if (b == p.B - 1) eptr[p.B] = off + prev_edges;
             }
@@ -1066,8 +1068,10 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     }
 }
 
-const void *roll_tile_kernel_fn(const DevParams &p) {
-    return p.path == kPathTile && p.tile_sym ? reinterpret_cast<const void *>(&gsm_roll_tile_kernel) : nullptr;
+const void *roll_tile_kernel_fn(const DevParams &p, bool slots) {
+    if (p.path != kPathTile || !p.tile_sym) return nullptr;
+    return slots ? reinterpret_cast<const void *>(&gsm_roll_tile_kernel<true>)
+                 : reinterpret_cast<const void *>(&gsm_roll_tile_kernel<false>);
 }
 
 const void *step_tile_kernel_fn() { return reinterpret_cast<const void *>(&gsm_step_tile_kernel); }
