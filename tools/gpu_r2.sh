@@ -22,12 +22,14 @@ for c in c2 c3 c4; do
 done
 timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench_h_driver.json 2> $O/bench_h_driver.err || exit 8
 timeout -k 10 300 python bench.py --no-roll --no-cpu-baseline > $O/bench_h_noroll.json 2> $O/bench_h_noroll.err || exit 8
+timeout -k 10 300 python bench.py --config c3 --no-roll --no-cpu-baseline > $O/bench_c3_noroll.json 2> $O/bench_c3_noroll.err || exit 8
+timeout -k 10 300 python bench.py --config c2 --no-roll --no-cpu-baseline > $O/bench_c2_noroll.json 2> $O/bench_c2_noroll.err || exit 8
 timeout -k 10 120 python bench.py --gpus 2 --steps 5 > $O/bench_gpus2.out 2>&1; echo "bench --gpus 2 on one GPU: exit $?" >> $O/bench_gpus2.out
 for c in h c2 c3 c4; do
   cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof_$c" -o run --output-format csv -- python "$GRAFT_REPO_ROOT/bench.py" --config $c --no-cpu-baseline > "$GRAFT_REPO_ROOT/$O/prof_$c.log" 2>&1 || exit 7
 done
 cd "$GRAFT_REPO_ROOT"
-for c in h c2 c3 c4 h_driver h_noroll; do
+for c in h c2 c3 c4 h_driver h_noroll c2_noroll c3_noroll; do
   python -c "import json;d=json.load(open('$O/bench_$c.json'));r=d['roofline'];print('$c',d['value'],'us/step',round(d['ms_per_step']*1e3,2),r['kernel'],r['mean_launch_us'],'us frac',r['frac'],'valu',r['valu_frac'],'issue',r.get('issue_frac'),'traffic',r['traffic'],'bounds',d['timed_region']['episode_boundaries'])"
 done
 tail -2 $O/bench_gpus2.out
