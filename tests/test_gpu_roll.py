@@ -183,3 +183,28 @@ def test_roll_replay_after_other_work(N, B):
     assert not env.roll_gave_up()
     _same(ref, env, "replay after eager work")
     env.close()
+
+
+@pytest.mark.parametrize("N,B", [(24, 8192), (3, 4096), (96, 1024)])
+def test_roll_episodes_match_chain(N, B):
+    """Three 100-step episodes replayed back to back (auto-resets inside each
+    launch, granule epochs advancing) leave every buffer exactly as the
+    per-step chain does — the BASELINE shapes at full size."""
+    T = 100
+    env, cfg = _env(n_agents=N, n_envs=B, episode_length=T)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    env.reset(seed=5)
+    env.capture(acts, T, slot=0, kernels="both")   # lagged chain (two-kernel chain on the tile path)
+    for _ in range(3):
+        env.replay(0)
+    torch.cuda.synchronize()
+    ref = {k: v.clone() for k, v in env.t.items()}
+    env.reset(seed=5)
+    env.capture(acts, T, slot=1, kernels="roll")
+    assert env.graph_is_rollout(1)
+    for _ in range(3):
+        env.replay(1)
+    torch.cuda.synchronize()
+    assert not env.roll_gave_up()
+    _same(ref, env, "3 episodes")
+    env.close()
