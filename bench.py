@@ -577,8 +577,9 @@ def run_rank(args):
                        "agents_per_step": agents,
                        "episode_length": EL, "mean_edges_per_env": round(total_edges / B, 2),
                        "parallelism": f"env-sharded x{world} (no data-path collective)",
-                       "launch": "eager" if args.eager else ("hip-graph per 100-step episode" + (
-                           ": all 100 steps in one fused rollout launch (state on chip, in-launch CSR prefix)"
+                       "launch": "eager" if args.eager else (f"hip-graphs of {chunk} steps" + (
+                           ": all steps of a graph in one fused rollout launch (state on chip, in-launch CSR "
+                           "prefix) + the last step's emit launch"
                            if roll else ", lagged emission (one launch per step)" if (seg_cfg and not args.unfused)
                            else ", step + emit launch per step"))},
             "timed_region": {"untimed_steps_before": P, "align_steps": A,
