@@ -490,6 +490,9 @@ def run_rank(args):
     sync()
     metrics = torch.zeros(3, dtype=torch.float64, device=dev)
 
+    # ragged: the assignment warm start's certified / solved counters, read
+    # around the timed region (outside it)
+    lsa0 = env.lsa_warm_stats() if (cfg.ragged and hasattr(env, "lsa_warm_stats")) else None
     if world > 1:
         dist.barrier()
     sync()
@@ -513,6 +516,7 @@ def run_rank(args):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    lsa1 = env.lsa_warm_stats() if lsa0 is not None else None
 
     # every rank's timed region; value uses the slowest (max over ranks)
     per_rank = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -593,6 +597,11 @@ def run_rank(args):
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if lsa1 is not None:   # rank 0's polygon/line envs over the timed region
+            hits, solved = lsa1[0] - lsa0[0], lsa1[1] - lsa0[1]
+            line["assignment"] = {"warm_start_certified": hits, "assignments_solved": solved,
+                                  "hit_rate": round(hits / solved, 6) if solved else None,
+                                  "scope": "rank 0, timed region; the rest are solved cold"}
         print(json.dumps(line), flush=True)
     env.close()
     if world > 1:
