@@ -135,7 +135,9 @@ def ragged_kernel_bytes(env, EL, action_bytes, total_edges):
     amortised over the episode; polygon/line envs also read and write their
     assignment warm-start state (f64 column dual + int32 matching per agent,
     when the warm start is on). emit: reads all E_max positions, the M row
-    masks, edge count and shape; writes edge_ptr and 12 B per edge."""
+    masks, edge count and shape; writes edge_ptr and 12 B per edge. lag: what
+    a lagged step kernel adds to the step (the emission less the collider and
+    target positions and the shape word the step reads anyway)."""
     import numpy as np
     sh = env.t["env_shape"].cpu().numpy()
     n, scn = (sh & 0xFF).astype(np.int64), sh >> 8
@@ -148,7 +150,8 @@ def ragged_kernel_bytes(env, EL, action_bytes, total_edges):
     warm = np.where(scn != 0, 2 * 12 * n, 0) if env.cfg.lsa_warm_start else 0
     step = float((reads + writes + reset + warm).sum()) + 4 * len(n) / 4
     emit = float((8 * Emax + 8 * M + 4 + 4 + 8).sum()) + 12 * total_edges
-    return step, emit
+    lag = emit - float((8 * (M + T) + 4).sum())
+    return step, emit, lag
 
 
 CONFIGS = {   # BASELINE.json configs runnable as a one-GPU bench line
@@ -584,7 +587,8 @@ def run_rank(args):
                        "launch": "eager" if args.eager else (f"hip-graphs of {chunk} steps" + (
                            ": all steps of a graph in one fused rollout launch (state on chip, in-launch CSR "
                            "prefix) + the last step's emit launch"
-                           if roll else ", lagged emission (one launch per step)" if (seg_cfg and not args.unfused)
+                           if roll else ", lagged emission (one launch per step)" if ((seg_cfg or cfg.ragged)
+                                                                                     and not args.unfused)
                            else ", step + emit launch per step"))},
             "timed_region": {"untimed_steps_before": P, "align_steps": A,
                              "episode_boundaries": boundaries_in(P, K, EL),
@@ -613,7 +617,7 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False):
     import torch
     L = args.kernel_launches
     seg = (N + cfg.n_obstacles) <= 64 and not cfg.ragged
-    lag = seg and not args.unfused and not roll   # segmented chains: lagged emission
+    lag = (seg or cfg.ragged) and not args.unfused and not roll   # segmented / ragged chains: lagged emission
     # the fused rollout: events around its launch of L steps (time per step)
     env.capture(actions, L, slot=3, kernels="roll" if roll else "lag" if lag else "step", time_ends=True)
     env.replay(3)
@@ -625,8 +629,10 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False):
     emit_ms = env.graph_kernel_ms(3)[1]
     edges_now = int(env.t["edge_ptr"][B].item())
     if cfg.ragged:
-        sb, eb = ragged_kernel_bytes(env, EL, 4, edges_now)
-        names = ("gsm_step_ragged_kernel", "gsm_emit_ragged_kernel")
+        sb, eb, lb = ragged_kernel_bytes(env, EL, 4, edges_now)
+        if lag:
+            sb += lb
+        names = ("gsm_step_ragged_kernel" + ("<lagged emission>" if lag else ""), "gsm_emit_ragged_kernel")
     elif roll:
         sb = roll_step_bytes(B, N, cfg.n_obstacles, EL, 4, edges_now, seg)
         eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)

@@ -716,7 +716,7 @@ static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_
     const bool lag_only = (flags & GSM_GRAPH_LAG_ONLY) != 0;
     const bool can_lag = gsm::lag_step_kernel_fn(h->dp) != nullptr;
     if (lag_only && (!can_lag || each || (flags & (GSM_GRAPH_STEP | GSM_GRAPH_EMIT | GSM_GRAPH_UNFUSED))))
-        return fail(h, GSM_EINVAL, "GSM_GRAPH_LAG_ONLY: segmented configs only, no other kernel/timing-each flags");
+        return fail(h, GSM_EINVAL, "GSM_GRAPH_LAG_ONLY: segmented / ragged configs only, no other kernel/timing-each flags");
     if (lag_only) kern = GSM_GRAPH_STEP;
     // lagged emission: step_0, lag_step_1 .. lag_step_{T-1}, emit_{T-1}
     const bool lag = lag_only || (can_lag && !each && kern == (GSM_GRAPH_STEP | GSM_GRAPH_EMIT) &&

@@ -137,7 +137,7 @@ const void *emit_kernel_fn(const DevParams &p);
 const void *step_seg_kernel_fn(const DevParams &p);
 // step kernel that emits the previous step's edges first (p.lag); nullptr
 // where the path has none (tile: measured no faster than its own emit
-// launch; ragged)
+// launch)
 const void *lag_step_kernel_fn(const DevParams &p);
 const void *lag_step_seg_kernel_fn(const DevParams &p);
 const void *emit_seg_kernel_fn(const DevParams &p);
@@ -148,6 +148,7 @@ size_t roll_kernel_lds(const DevParams &p);
 const void *roll_tile_kernel_fn(const DevParams &p, bool slots);   // nullptr unless p.tile_sym
 size_t roll_tile_kernel_lds(const DevParams &p);
 const void *step_ragged_kernel_fn();
+const void *lag_step_ragged_kernel_fn();   // kLag: the previous step's emission first
 const void *step_tile_kernel_fn();
 const void *emit_tile_kernel_fn();
 int block_threads(const DevParams &p);

@@ -12,10 +12,10 @@
 //   ragged     polygon / line / mixed: one wave per env, per-env shape,
 //              per-step assignment (gsm_ragged_kernels.hip).
 //
-// Inside a graph chain the segmented family fuses the emitter of step t
-// into the step kernel of step t+1 ("lagged emission"): the
-// edges of step t are functions of the positions and row masks that step t+1
-// loads anyway, so the chain is step_0, lag_step_1, ..., lag_step_{T-1},
+// Inside a graph chain the segmented and ragged families fuse the emitter of
+// step t into the step kernel of step t+1 ("lagged emission"):
+// the edges of step t are functions of the positions and row masks that step
+// t+1 loads anyway, so the chain is step_0, lag_step_1, ..., lag_step_{T-1},
 // emit_{T-1}: one launch per step instead of two.
 //
 // Launches go through hipLaunchKernel with the family's kernel pointers; the
@@ -38,6 +38,7 @@ const void *step_kernel_fn(const DevParams &p) {
     return step_seg_kernel_fn(p);
 }
 const void *lag_step_kernel_fn(const DevParams &p) {
+    if (p.path == kPathRagged) return lag_step_ragged_kernel_fn();
     return p.path == kPathSeg ? lag_step_seg_kernel_fn(p) : nullptr;
 }
 const void *emit_kernel_fn(const DevParams &p) {
@@ -49,9 +50,12 @@ const void *emit_kernel_fn(const DevParams &p) {
 #define GSM_LDS_PAD 0
 #endif
 size_t step_kernel_lds(const DevParams &p) {
-    // segmented: + per-wave edge sums and (lagged emission) per-wave prefix words
-    return p.path == kPathTile ? (size_t)p.wave_lds_step
-                               : (size_t)kWavesPerBlock * p.wave_lds_step + 32 + GSM_LDS_PAD;
+    // segmented / ragged: + per-wave edge sums and (lagged emission) per-wave prefix words;
+    // ragged: + the lagged emission's staged inputs (gsm_ragged_kernels.hip RaggedLagLds:
+    // counters, 4 x 64 row masks, 4 x E_max positions)
+    if (p.path == kPathTile) return (size_t)p.wave_lds_step;
+    const size_t lag = p.path == kPathRagged ? 64 + 8 * kWave * kWavesPerBlock + 8 * (size_t)kWavesPerBlock * p.E : 0;
+    return (size_t)kWavesPerBlock * p.wave_lds_step + 32 + lag + GSM_LDS_PAD;
 }
 size_t emit_kernel_lds(const DevParams &p) {
     return p.path == kPathTile ? (size_t)p.wave_lds_emit : (size_t)kWavesPerBlock * p.wave_lds_emit + 16;

@@ -542,7 +542,10 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
 // ---------------------------------------------------------------------------
 // step kernel
 // ---------------------------------------------------------------------------
-__device__ int ragged_env_step(const DevParams &p, const int b, const int lane, unsigned char *lds) {
+// `stage` runs once the step's own loads of the env state have been issued
+// (the lagged kernel stages the previous step's emission inputs there)
+template <class Stage>
+__device__ int ragged_env_step(const DevParams &p, const int b, const int lane, unsigned char *lds, Stage &&stage) {
     const int Nmax = p.N, Tmax = p.T, Emax = p.E, Mmax = p.M;
     const int64_t eb = b;
     const LsaLds s_lsa = lsa_lds(lds, Nmax);                    // assignment scratch
@@ -583,6 +586,7 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
         if (lane < s.T) tp = pos_b[Nmax + lane];
         if (lane < s.N) v = p.vel[eb * Nmax + lane];
     }
+    stage();
 
     bool done = false;
     if (p.mode == kModeStep) {
@@ -792,17 +796,122 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
 #else
 #define GSM_RAGGED_ATTR
 #endif
+__device__ void ragged_env_emit_rows(const DevParams &p, const int b, const int lane, const int64_t off,
+                                     const float2 *s_pos, const RShape &s, uint64_t mask, const EdgeSink &out);
+
+// kLag (graph chains, gsm_abi.hip capture_impl): the kernel also emits the
+// edges of the PREVIOUS step of its workgroup's envs — functions of this
+// launch's input positions, row masks and shapes — into the previous step's
+// outputs (p.lag), at the offsets given by the previous launch's
+// per-workgroup sums (p.lag.block_sum, env-block order; this launch writes
+// its own sums to the other half). This replaces the separate emit launch of
+// that step. The kernel's time is set by its slowest env's assignment
+// (DESIGN.md §4), so the emission is kept off that env's path: each wave
+// stages its env's emission inputs in LDS (while its own state loads are in
+// flight), and the waves that finish their step first claim the workgroup's
+// four emissions (an LDS counter) — normally the slowest wave claims none.
+struct RaggedLagLds {
+    int *job, *ready;   // next emission to claim; per wave: inputs staged
+    int *cnt, *shape;   // per wave: previous edge count and shape word
+    uint64_t *rm;       // [4][64] previous row masks
+    float2 *pos;        // [4][E_max] previous positions
+};
+// at smem + 4 * wave_lds_step + 32 (gsm_kernels.hip step_kernel_lds)
+__device__ __forceinline__ RaggedLagLds ragged_lag_lds(unsigned char *base, int E) {
+    RaggedLagLds l;
+    l.job = (int *)base;
+    l.ready = l.job + 4;
+    l.cnt = l.job + 8;
+    l.shape = l.job + 12;
+    l.rm = (uint64_t *)(base + 64);
+    l.pos = (float2 *)(base + 64 + 8 * kWave * kWavesPerBlock);
+    (void)E;
+    return l;
+}
+
+template <bool kLag>
 __global__ __launch_bounds__(kBlock) GSM_RAGGED_ATTR void gsm_step_ragged_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: env shape, loops and assignment state stay scalar
     // env block of this workgroup (mixed: heaviest first, gsm_abi.hip update_block_order)
     const int blk = p.block_order ? p.block_order[blockIdx.x] : (int)blockIdx.x;
     const int b = blk * kWavesPerBlock + wave;
+    const int first = blk * kWavesPerBlock;
+    const int nlive = min(kWavesPerBlock, p.B - first);
+    int *s_bc = (int *)(smem + kWavesPerBlock * p.wave_lds_step);
+    const RaggedLagLds L = ragged_lag_lds(smem + kWavesPerBlock * p.wave_lds_step + 32, p.E);
+    int32_t sh = 0;
+    uint64_t rm = 0;
+    float2 q0 = make_float2(0.0f, 0.0f), q1 = q0;
+    int ck = 0;
+    if constexpr (kLag) {
+        // the emission inputs (E_max <= 3 * 32 rows: two per lane), loaded
+        // before the step's: the step's first wait covers them
+        const int64_t eb = b < p.B ? b : 0;
+        sh = p.env_shape[eb];
+        rm = lane < p.M ? p.row_mask[eb * p.M + lane] : 0ull;
+        q0 = lane < p.E ? p.pos[eb * p.E + lane] : q0;
+        q1 = lane + kWave < p.E ? p.pos[eb * p.E + lane + kWave] : q1;
+        ck = p.lag.edge_count[eb];
+        if (threadIdx.x < 2 * kWavesPerBlock) L.job[threadIdx.x] = 0;   // job and ready[]
+        // LDS only: the barrier does not wait for the loads above
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+    // the wave's own env's inputs into LDS, before its step overwrites them
+    // (every read of a previous edge count or row mask precedes that write)
+    auto stage = [&]() {
+        if constexpr (kLag) {
+            float2 *sp = L.pos + wave * p.E;
+            if (lane < p.E) sp[lane] = q0;
+            if (lane + kWave < p.E) sp[lane + kWave] = q1;
+            L.rm[wave * kWave + lane] = rm;
+            if (lane == 0) {
+                L.cnt[wave] = ck;
+                L.shape[wave] = sh;
+            }
+            __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the rows land before the flag
+            if (lane == 0) __hip_atomic_store(&L.ready[wave], 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+    };
     int edges = 0;
     GSM_RSTAMP(p, b, 8);
-    if (b < p.B) edges = ragged_env_step(p, b, lane, smem + wave * p.wave_lds_step);
+    if (b < p.B) edges = ragged_env_step(p, b, lane, smem + wave * p.wave_lds_step, stage);
+    else stage();
     GSM_RSTAMP(p, b, 9);
-    int *s_bc = (int *)(smem + kWavesPerBlock * p.wave_lds_step);
+    if constexpr (kLag) {
+        // claim the workgroup's emissions until none is left
+        int j = lane == 0 ? __hip_atomic_fetch_add(L.job, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
+        j = __builtin_amdgcn_readfirstlane(j);
+        if (j < nlive) {
+            // every wave's inputs staged (set early in every wave's step;
+            // bounded wait)
+            for (int spin = 0; spin < (1 << 20); ++spin) {
+                const int r = lane < nlive ? __hip_atomic_load(&L.ready[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : 1;
+                if (__all(r != 0)) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+            // exclusive prefix of the preceding workgroups' previous sums
+            int acc = 0;
+#pragma unroll 8
+            for (int k = lane; k < blk; k += kWave) acc += p.lag.block_sum[k];
+            const int64_t base = wave_sum(acc);
+            const int cl = lane < nlive ? L.cnt[lane] : 0;
+            while (j < nlive) {
+                const int bj = first + j;
+                const int64_t off = base + wave_sum(lane < j ? cl : 0);
+                if (lane == 0) {
+                    p.lag.edge_ptr[bj] = off;
+                    if (bj == p.B - 1) p.lag.edge_ptr[p.B] = off + __builtin_amdgcn_readlane(cl, j);
+                }
+                const int32_t shj = L.shape[j];
+                const RShape s = make_shape(p, shj & 0xFF, shj >> 8);
+                ragged_env_emit_rows(p, bj, lane, off, L.pos + j * p.E, s, lane < s.M ? L.rm[j * kWave + lane] : 0ull,
+                                     EdgeSink{p.lag.edge_index, p.lag.edge_attr, p.lag.cap});
+                j = lane == 0 ? __hip_atomic_fetch_add(L.job, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0;
+                j = __builtin_amdgcn_readfirstlane(j);
+            }
+        }
+    }
     if (lane == 0) s_bc[wave] = edges;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -815,31 +924,28 @@ __global__ __launch_bounds__(kBlock) GSM_RAGGED_ATTR void gsm_step_ragged_kernel
 // ---------------------------------------------------------------------------
 // edge emitter
 // ---------------------------------------------------------------------------
-__device__ void ragged_env_emit(const DevParams &p, const int b, const int lane, const int64_t off,
-                                unsigned char *lds) {
-    const int Nmax = p.N, Tmax = p.T, Emax = p.E, Mmax = p.M;
+// env b's edges at global offset `off` from its positions staged in LDS
+// (s_pos, all E_max rows) and its collider lanes' row masks
+__device__ void ragged_env_emit_rows(const DevParams &p, const int b, const int lane, const int64_t off,
+                                     const float2 *s_pos, const RShape &s, const uint64_t mask,
+                                     const EdgeSink &out) {
+    const int Nmax = p.N, Tmax = p.T, Emax = p.E;
     const int64_t eb = b;
-    float2 *s_pos = (float2 *)lds;
-    const int32_t sh = p.env_shape[b];
-    const RShape s = make_shape(p, sh & 0xFF, sh >> 8);
-    for (int q = lane; q < Emax; q += kWave) s_pos[q] = p.pos[eb * Emax + q];
-    wave_sync();
-    int32_t *const src = p.edge_index;
-    int32_t *const dst = p.edge_index + p.edge_capacity;
+    int32_t *const src = out.index;
+    int32_t *const dst = out.index + out.cap;
     const int32_t g0 = (int32_t)(eb * Emax);
-    const uint64_t mask = lane < s.M ? p.row_mask[eb * Mmax + lane] : 0ull;
     const int cnt = __popcll(mask) + (lane < s.N ? s.Tper : 0);
     const int incl = wave_scan(cnt);
     const int agent_total = s.N > 0 ? __builtin_amdgcn_readlane(incl, s.N - 1) : 0;
     // row order: agent rows, target rows (N*Tper edges), obstacle rows
     int64_t o = off + (incl - cnt) + (lane >= s.N ? s.N * s.Tper : 0);
     auto put = [&](int a_row, float2 a, int d_row) {
-        if (o < p.edge_capacity) {   // redirected outputs may be smaller than the worst case
+        if (o < out.cap) {   // redirected outputs may be smaller than the worst case
             const float2 q = s_pos[d_row];
             const float dx = a.x - q.x, dy = a.y - q.y;
             src[o] = g0 + a_row;
             dst[o] = g0 + d_row;
-            p.edge_attr[o] = sqrtf(dx * dx + dy * dy);
+            out.attr[o] = sqrtf(dx * dx + dy * dy);
         }
         ++o;
     };
@@ -884,6 +990,18 @@ __device__ void ragged_env_emit(const DevParams &p, const int b, const int lane,
     }
 }
 
+__device__ void ragged_env_emit(const DevParams &p, const int b, const int lane, const int64_t off,
+                                unsigned char *lds, const EdgeSink &out) {
+    const int64_t eb = b;
+    float2 *s_pos = (float2 *)lds;
+    const int32_t sh = p.env_shape[b];
+    const RShape s = make_shape(p, sh & 0xFF, sh >> 8);
+    for (int q = lane; q < p.E; q += kWave) s_pos[q] = p.pos[eb * p.E + q];
+    const uint64_t mask = lane < s.M ? p.row_mask[eb * p.M + lane] : 0ull;
+    wave_sync();
+    ragged_env_emit_rows(p, b, lane, off, s_pos, s, mask, out);
+}
+
 __global__ __launch_bounds__(kBlock) void gsm_emit_ragged_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -904,10 +1022,11 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_ragged_kernel(DevParams p) {
         p.edge_ptr[b] = off;
         if (b == p.B - 1) p.edge_ptr[p.B] = off + p.edge_count[b];
     }
-    ragged_env_emit(p, b, lane, off, smem + wave * p.wave_lds_emit);
+    ragged_env_emit(p, b, lane, off, smem + wave * p.wave_lds_emit, EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity});
 }
 
-const void *step_ragged_kernel_fn() { return reinterpret_cast<const void *>(&gsm_step_ragged_kernel); }
+const void *step_ragged_kernel_fn() { return reinterpret_cast<const void *>(&gsm_step_ragged_kernel<false>); }
+const void *lag_step_ragged_kernel_fn() { return reinterpret_cast<const void *>(&gsm_step_ragged_kernel<true>); }
 const void *emit_ragged_kernel_fn() { return reinterpret_cast<const void *>(&gsm_emit_ragged_kernel); }
 
 // Host side: the tables come from float64 libm and are rounded to fp32 once,

@@ -223,15 +223,15 @@ int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream);
  * every kernel, GSM_GRAPH_TIME_ENDS brackets the whole graph (per-kernel
  * means over back-to-back launches, no event nodes between kernels).
  * A graph running only GSM_GRAPH_EMIT re-emits the current step's edges.
- * Segmented configs (navigation, N + No <= 64) chain the two kernels with
- * lagged emission: step j+1's kernel first emits step j's edges (they depend
+ * Segmented (navigation, N + No <= 64) and ragged (polygon / line / mixed)
+ * configs chain the two kernels with lagged emission: step j+1's kernel first emits step j's edges (they depend
  * only on its input positions and row masks), so a step is one launch and a
  * final emit launch ends the graph; every step's outputs are complete when
  * the graph has run, exactly as with the two-kernel chain (the library
  * allocates one n_blocks int32 buffer for this on first use).
  * GSM_GRAPH_UNFUSED forces the two-kernel chain (TIME_EACH implies it);
  * GSM_GRAPH_LAG_ONLY builds n_steps lagged step kernels and nothing else
- * (a timing tool: the last step's edges are left unemitted; segmented only).
+ * (a timing tool: the last step's edges are left unemitted; segmented / ragged only).
  * Graphs are dropped by gsm_bind and by a reseed to a different seed. */
 #define GSM_GRAPH_SLOTS 4
 #define GSM_GRAPH_STEP 1

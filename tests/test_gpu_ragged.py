@@ -186,6 +186,72 @@ def test_graph_replay_equals_eager():
     env.close()
 
 
+@pytest.mark.parametrize("scenario,N,B,T", [("mixed", 24, 8192, 7), ("mixed", 24, 257, 6), ("polygon", 12, 130, 5),
+                                             ("line", 9, 64, 4)])
+def test_lagged_chain_equals_eager(scenario, N, B, T):
+    """Ragged graph chains emit step j's edges from step j+1's kernel (lagged
+    emission, heaviest-first workgroup order for mixed): every state and output
+    buffer as after eager steps and the two-kernel chain, odd and even chain
+    lengths, partial workgroups, auto-resets (episode length 3); the bound
+    edge-sum buffer then re-emits the same edges."""
+    env, rcfg = _renv(scenario=scenario, n_agents=N, n_envs=B, seed=8, episode_length=3)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    keys = ("pos", "vel", "step_count", "episode", "node_feat", "reward", "cost", "done", "edge_count",
+            "edge_ptr", "ep_acc", "ep_last", "row_mask", "assign", "env_shape")
+    env.reset(seed=8)
+    for t in range(T):
+        env.step(acts[t], sync_edges=False)
+    torch.cuda.synchronize()
+    eager = {k: v.clone() for k, v in env.t.items()}
+    n = int(eager["edge_ptr"][-1])
+    for kernels, slot in (("both", 0), ("unfused", 1)):
+        env.reset(seed=8)
+        env.capture(acts, T, slot=slot, kernels=kernels)
+        env.t["edge_index"].fill_(-7)
+        env.replay(slot)
+        torch.cuda.synchronize()
+        for k in keys:
+            assert torch.equal(eager[k], env.t[k]), (kernels, k)
+        assert torch.equal(eager["edge_index"][:, :n], env.t["edge_index"][:, :n]), kernels
+        assert torch.equal(eager["edge_attr"][:n], env.t["edge_attr"][:n]), kernels
+        env.t["edge_index"].zero_()
+        env.capture(None, 1, slot=3, kernels="emit")
+        env.replay(3)
+        torch.cuda.synchronize()
+        assert torch.equal(eager["edge_ptr"], env.t["edge_ptr"]), kernels
+        assert torch.equal(eager["edge_index"][:, :n], env.t["edge_index"][:, :n]), kernels
+    env.close()
+
+
+def test_lagged_chain_every_step_into_rollout_slots():
+    """capture_into on a mixed config: the lagged chain writes slot j's edges
+    from step j+1's kernel; every slot equals eager step_into's."""
+    from gsmarl_amd import EnvConfig, GpuBatchEnv, GraphRolloutBuffer
+    B, N, T = 300, 24, 7
+    kw = dict(scenario="mixed", n_agents=N, n_envs=B, seed=4, episode_length=4)
+    env, ref = GpuBatchEnv(EnvConfig(**kw), DEV), GpuBatchEnv(EnvConfig(**kw), DEV)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    gb = GraphRolloutBuffer(env, episode_length=T)
+    eb = GraphRolloutBuffer(ref, episode_length=T)
+    gb.reset(seed=4)
+    gb.capture(acts)
+    assert not env.graph_is_rollout(0)
+    gb.replay()
+    eb.reset(seed=4)
+    for t in range(T):
+        eb.insert(acts[t])
+    torch.cuda.synchronize()
+    for k in ("node_feat", "reward", "cost", "done", "edge_ptr", "edge_count", "assign"):
+        assert torch.equal(getattr(gb, k), getattr(eb, k)), k
+    for t in range(T + 1):
+        n = int(gb.edge_ptr[t, B])
+        assert torch.equal(gb.edge_index[t][:, :n], eb.edge_index[t][:, :n]), t
+        assert torch.equal(gb.edge_attr[t][:n], eb.edge_attr[t][:n]), t
+    assert not bool(gb.overflowed())
+    env.close()
+    ref.close()
+
+
 def test_navigation_env_matches_navigation_batch():
     """A navigation env inside a mixed batch lays out exactly like the same
     env id of a plain navigation batch (different kernels, same contract)."""
