@@ -808,7 +808,7 @@ template <bool kSlots>   // per-step outputs at base + k * stride (a rollout buf
 __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int b = blockIdx.x;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
     const int N = p.N, E = p.E, W = p.W, M = p.M;
     float2 *s_pos = (float2 *)smem;           // [E]
     float2 *s_vel = s_pos + E;                // [N]
