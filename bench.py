@@ -266,6 +266,7 @@ VALU_ISSUE_CYCLES = 2.8   # per wave64 VALU instruction and SIMD
 SALU_ISSUE_CYCLES = 2.55  # per SALU instruction and SIMD
 N_SIMDS = 1024            # 256 CUs x 4 SIMDs
 CLOCK_GHZ = 2.0           # measured shader clock under load
+LATENCY_BELOW = 0.6       # issue and HBM fractions both below: latency-bound
 
 
 def pmc_entry(key):
@@ -676,8 +677,12 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False):
                     model=f"{VALU_ISSUE_CYCLES} / {SALU_ISSUE_CYCLES} SIMD cycles per VALU / SALU instruction "
                           f"(measured marginal cost) x {N_SIMDS} SIMDs at {CLOCK_GHZ} GHz (DESIGN.md §5)")
     # what binds the kernel: instruction issue (VALU + SALU) or HBM bandwidth;
-    # achieved / frac stay the HBM figures (algorithmic bytes / time / peak)
+    # when neither fills even LATENCY_BELOW of its peak, one wave's dependent
+    # chain sets the time (C4's tied assignment, a lagged chain at one wave per
+    # SIMD: DESIGN.md §4/§5). achieved / frac stay the HBM figures
     bound = "issue" if valu and valu["issue_frac"] > hbm_frac else "hbm"
+    if valu and max(valu["issue_frac"], hbm_frac) < LATENCY_BELOW:
+        bound = "latency"
     roofline = dict(kernel=k["kernel"], bound=bound, achieved=round(k["gbs"], 1), peak=HBM_PEAK_GBS,
                     unit="GB/s", frac=round(hbm_frac, 4), hbm_frac=round(hbm_frac, 4),
                     valu_frac=valu["frac"] if valu else None,
