@@ -244,17 +244,31 @@ def host_cores():
     return max(1, min(16, n, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
 
 
-def kernel_src_hash():
-    """Hash of the kernel sources (gs-marl_amd/csrc/*.hip, *.h): PMC figures
-    are injected into a bench line only when they were collected on exactly
-    these sources (tools/pmc_traffic.py records the hash)."""
+def code_object_hash(lib_path=None):
+    """Hash of the gfx950 device code the bench runs: the `.hip_fatbin`
+    section of the built libgsm.so (the offload bundle of every kernel). PMC
+    figures are injected into a bench line only when they were collected on
+    exactly this code (tools/pmc_traffic.py records the hash); edits to host
+    code, comments or tools leave it unchanged."""
     import hashlib
-    h = hashlib.sha256()
-    for p in sorted((ROOT / "gs-marl_amd" / "csrc").iterdir()):
-        if p.suffix in (".hip", ".h"):
-            h.update(p.name.encode())
-            h.update(p.read_bytes())
-    return h.hexdigest()[:16]
+    import struct
+    if lib_path is None:
+        from gsmarl_amd import _lib
+        lib_path = _lib.LIB_PATH
+    data = Path(lib_path).read_bytes()
+    # ELF64 little-endian: section headers, then the section-name string table
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", data, 0x3A)
+    def sec(i):
+        name, _, _, _, off, size = struct.unpack_from("<IIQQQQ", data, shoff + i * shentsize)
+        return name, off, size
+    _, stroff, _ = sec(shstrndx)
+    for i in range(shnum):
+        name, off, size = sec(i)
+        end = data.index(b"\0", stroff + name)
+        if data[stroff + name:end] == b".hip_fatbin":
+            return hashlib.sha256(data[off:off + size]).hexdigest()[:16]
+    raise RuntimeError(f"{lib_path}: no .hip_fatbin section")
 
 
 PMC_FILE = ROOT / "profiles" / "pmc_kernels.json"
@@ -272,16 +286,16 @@ LATENCY_BELOW = 0.6       # issue and HBM fractions both below: latency-bound
 def pmc_entry(key):
     """(entry, note) for kernel `key` from profiles/pmc_kernels.json: HBM
     bytes per launch (2 x FETCH_SIZE + WRITE_SIZE, gfx950 correction) and
-    VALU/SALU instructions per launch. None when absent or collected on other
-    kernel sources than the ones built here (stale figures are never used)."""
+    VALU/SALU instructions per launch. None when absent or collected on
+    another build of the device code (stale figures are never used)."""
     if not PMC_FILE.exists():
         return None, "no profiles/pmc_kernels.json"
     try:
         d = json.loads(PMC_FILE.read_text())
     except Exception as e:   # a broken file must not break the bench line
         return None, f"unreadable pmc file: {e}"
-    if d.get("src_hash") != kernel_src_hash():
-        return None, "stale: profiles/pmc_kernels.json was collected on other kernel sources"
+    if d.get("code_object_hash") != code_object_hash():
+        return None, "stale: profiles/pmc_kernels.json was collected on another build of the kernels"
     e = d.get("entries", {}).get(key)
     return (e, "ok") if e else (None, f"no PMC entry for {key}")
 

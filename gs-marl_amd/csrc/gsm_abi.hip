@@ -10,6 +10,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -37,9 +38,19 @@ struct gsm_handle {
         int kern = 0;
         bool each = false;
         uint64_t *gran = nullptr;     // fused rollout: epoch word, then the edge-sum granules
-        bool roll = false;            // the graph is one rollout launch (+ the final emit)
+        bool roll = false;            // the graph is one rollout launch
+        // A rollout graph without timing events is one kernel node: launched
+        // directly (the same kernel, grid and arguments) — a plain dispatch
+        // costs the host less than a graph launch; the graph is kept for
+        // gsm_graph_info and as the record of what runs.
+        bool direct = false;
+        const void *fn = nullptr;
+        dim3 grid, block;
+        unsigned lds = 0;
+        gsm::DevParams args;
     } slots[GSM_GRAPH_SLOTS];
     uint32_t *roll_status = nullptr;  // fused rollout: a bounded wait gave up (sticky until read)
+    void *edge_scratch = nullptr;     // fused rollout in the bound buffers: edges of all but the last step
 };
 
 namespace {
@@ -350,6 +361,8 @@ void drop_slot(gsm_handle::Slot &s) {
     if (s.gran) (void)hipFree(s.gran);
     s.gran = nullptr;
     s.roll = false;
+    s.direct = false;
+    s.fn = nullptr;
     s.exec = nullptr;
     s.graph = nullptr;
     s.events.clear();
@@ -363,6 +376,14 @@ void drop_graph(gsm_handle *h) {
 }
 
 bool bad_slot(int32_t slot) { return slot < 0 || slot >= GSM_GRAPH_SLOTS; }
+
+// the status word is read by agent-scope loads in the kernels: cleared by the
+// same kind of stores (gsm_kernels.hip launch_granule_init), synchronously
+hipError_t clear_status(gsm_handle *h) {
+    hipError_t e = gsm::launch_granule_init(h->roll_status, 16, 0u, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    return e;
+}
 
 }  // namespace
 
@@ -490,6 +511,38 @@ int gsm_observe(gsm_handle *h, void *stream) {
     return launch(h, GSM_MODE_OBSERVE, nullptr, 0, nullptr, 0, as_stream(stream));
 }
 
+// state copies (gsm_state): direction 0 = bound -> caller, 1 = caller -> bound
+static int copy_state(gsm_handle *h, const gsm_state *st, int dir, hipStream_t s) {
+    if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
+    if (!h->bound) return fail(h, GSM_ESTATE, "gsm_bind has not been called");
+    if (!st) return fail(h, GSM_EINVAL, "state is NULL");
+    const gsm::DevParams &p = h->dp;
+    const size_t B = (size_t)p.B;
+    struct F { void *caller, *bound; size_t bytes; } f[] = {
+        {st->pos, p.pos, B * p.E * 8}, {st->vel, p.vel, B * p.N * 8},
+        {st->step_count, p.step_count, B * 4}, {st->episode, p.episode, B * 4},
+        {st->ep_acc, p.ep_acc, B * 8}, {st->ep_last, p.ep_last, B * 8},
+        {st->env_shape, p.env_shape, B * 4},
+    };
+    for (const F &x : f) {
+        if (!x.caller || !x.bound) continue;   // skipped (env_shape: navigation binds none)
+        const hipError_t e = dir ? hipMemcpyAsync(x.bound, x.caller, x.bytes, hipMemcpyDeviceToDevice, s)
+                                 : hipMemcpyAsync(x.caller, x.bound, x.bytes, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return hip_fail(h, e, "hipMemcpyAsync (state)");
+    }
+    return GSM_OK;
+}
+
+int gsm_get_state(gsm_handle *h, const gsm_state *out, void *stream) {
+    return copy_state(h, out, 0, as_stream(stream));
+}
+
+int gsm_set_state(gsm_handle *h, const gsm_state *in, void *stream) {
+    const int rc = copy_state(h, in, 1, as_stream(stream));
+    if (rc) return rc;
+    return launch(h, GSM_MODE_OBSERVE, nullptr, 0, nullptr, 0, as_stream(stream));
+}
+
 int gsm_step_into(gsm_handle *h, const void *actions, int action_fmt, const gsm_outputs *out, void *stream) {
     if (!out) return fail(h, GSM_EINVAL, "outputs is NULL");
     return launch(h, GSM_MODE_STEP, actions, action_fmt, nullptr, 0, as_stream(stream), out);
@@ -514,6 +567,9 @@ int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t 
 
 int gsm_graph_capture_into(gsm_handle *h, int32_t slot, const void *actions, int64_t stride,
                            int32_t n_actions, int32_t n_steps, int action_fmt, const gsm_outputs *per_step) {
+    if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
+    if (!h->bound) return fail(h, GSM_ESTATE, "gsm_bind has not been called");
+    if (bad_slot(slot)) return fail(h, GSM_EINVAL, "bad graph slot");
     if (!per_step) return fail(h, GSM_EINVAL, "per_step outputs is NULL");
     // one rollout launch when the config has a rollout kernel and the slots
     // sit at constant strides (a rollout buffer), else the per-step chain
@@ -524,12 +580,17 @@ int gsm_graph_capture_into(gsm_handle *h, int32_t slot, const void *actions, int
 
 
 
-// Fused rollout graph (GSM_GRAPH_ROLL): a zeroing memset of the granules, ONE
-// gsm_roll_seg_kernel launch for all n_steps steps (it emits the edges of all
-// but the last), the emit launch for the last step. Every output equals the
-// lagged chain's.
+// Fused rollout graph (GSM_GRAPH_ROLL): ONE gsm_roll_seg_kernel /
+// gsm_roll_tile_kernel launch for all n_steps steps and all their edges (the
+// last step's emitted by a tail iteration; that launch also advances the
+// granule epoch). Every output equals the lagged chain's.
 static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_t stride, int32_t n_actions,
                         int32_t n_steps, int action_fmt, int flags, const gsm_outputs *per_step, bool fallback) {
+    // every caller checks these first; repeated so that no path reaches the
+    // slot or the bound buffers without them
+    if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
+    if (!h->bound) return fail(h, GSM_ESTATE, "gsm_bind has not been called");
+    if (bad_slot(slot)) return fail(h, GSM_EINVAL, "bad graph slot");
     if (flags & ~(GSM_GRAPH_ROLL | GSM_GRAPH_TIME_ENDS))
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL combines with GSM_GRAPH_TIME_ENDS only");
     if (!actions || n_actions < 1 || stride < 0) return fail(h, GSM_EINVAL, "bad capture arguments");
@@ -550,7 +611,7 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     // step k's outputs at base + k * stride (a rollout buffer's slots) or all
     // in the bound buffers
     gsm::DevParams::RollOut ro{p.node_feat, p.reward, p.cost, p.done, p.edge_count, p.edge_ptr, p.edge_index,
-                               p.edge_attr, 0, 0, 0, 0, 0, 0, 0, p.edge_capacity};
+                               p.edge_attr, 0, 0, 0, 0, 0, 0, 0, p.edge_capacity, nullptr, nullptr};
     if (per_step) {
         int64_t cost_s = 0;
         bool ok = slot_field(per_step, n_steps, &gsm_outputs::node_feat, &ro.nf, &ro.nf_s) &&
@@ -589,28 +650,61 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         if (fallback) return kRollIneligible;
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: the batch exceeds one residency round of the rollout kernel");
     }
-    gsm_handle::Slot &sl = h->slots[slot];
-    drop_slot(sl);
+    const int K = n_steps;
+    // tags carry the step in 12 bits (one env per wave) or 16 (tile); checked
+    // before the slot's graph is dropped
+    const int max_k = tile ? 65535 : gsm::kXferMaxSteps;
+    if (K > max_k) {
+        if (fallback) return kRollIneligible;
+        return fail(h, GSM_EINVAL, tile ? "GSM_GRAPH_ROLL: n_steps must be <= 65535"
+                                        : "GSM_GRAPH_ROLL: n_steps must be <= 4095");
+    }
+    // one env per wave: per-wave granules, groups of 64 waves (at most 128
+    // groups: one residency round holds <= 8192 waves)
+    const int xW = nb * gsm::kWavesPerBlock, xNG = (xW + gsm::kWave - 1) / gsm::kWave;
+    if (!tile && xNG > 2 * gsm::kWave) {
+        if (fallback) return kRollIneligible;
+        return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: more than 8192 envs in one rollout launch");
+    }
     if (!h->roll_status) {
         e = hipMalloc(&h->roll_status, 16);
-        if (e == hipSuccess) e = hipMemset(h->roll_status, 0, 16);
+        if (e == hipSuccess) e = clear_status(h);
         if (e != hipSuccess) { h->roll_status = nullptr; return hip_fail(h, e, "hipMalloc (rollout status)"); }
     }
     if (!h->cap_stream) {
         e = hipStreamCreateWithFlags(&h->cap_stream, hipStreamNonBlocking);
         if (e != hipSuccess) return hip_fail(h, e, "hipStreamCreate");
     }
-    const int K = n_steps;
-    if (K > 65535) return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: n_steps must be <= 65535");
-    // a 16-byte header (the launch epoch), then aggregates [K][nb] and
-    // inclusive prefixes [K][nb] (look-back); zeroed once here — granules are
-    // tagged with the launch epoch, so replays never clear them
-    const size_t gran_alloc = 16 + 2 * (size_t)K * nb * sizeof(uint64_t);
+    // in the bound buffers, the edges of every step but the last go to a
+    // scratch of the bound capacity (DevParams::RollOut); allocated once
+    if (!per_step && !h->edge_scratch) {
+        e = hipMalloc(&h->edge_scratch, 12 * (size_t)h->sz.edge_capacity);
+        if (e != hipSuccess) {
+            h->edge_scratch = nullptr;
+            if (fallback) return kRollIneligible;
+            return hip_fail(h, e, "hipMalloc (rollout edge scratch)");
+        }
+    }
+    gsm_handle::Slot &sl = h->slots[slot];
+    drop_slot(sl);
+    // a 16-byte header (the launch epoch), then one env per wave: per-wave
+    // counts [K][xW] and group sums [K][xNG] (32-bit granules); tile: aggregates
+    // [K][nb] and inclusive prefixes [K][nb] (look-back). Zeroed once here —
+    // granules are tagged with the launch epoch, so replays never clear them
+    const size_t gran_alloc = tile ? 16 + 2 * (size_t)K * nb * sizeof(uint64_t)
+                                   : 16 + (size_t)K * (xW + xNG) * sizeof(uint32_t);
     e = hipMalloc(&sl.gran, gran_alloc);
-    if (e != hipSuccess) { sl.gran = nullptr; return hip_fail(h, e, "hipMalloc (rollout granules)"); }
-    e = hipMemsetAsync(sl.gran, 0, gran_alloc, h->cap_stream);
+    if (e != hipSuccess) {
+        sl.gran = nullptr;
+        if (fallback) return kRollIneligible;   // the per-step chain needs no granules
+        return hip_fail(h, e, "hipMalloc (rollout granules)");
+    }
+    // every capture starts its granules at a new epoch (process-wide counter),
+    // written, like the zeros, by agent-scope stores (launch_granule_init)
+    static std::atomic<uint32_t> next_epoch{0};
+    e = gsm::launch_granule_init(sl.gran, gran_alloc, next_epoch.fetch_add(1) & 0xffffu, h->cap_stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->cap_stream);
-    if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipMemset (rollout granules)"); }
+    if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "rollout granule init"); }
     const bool ends = (flags & GSM_GRAPH_TIME_ENDS) != 0;
     sl.events.resize(ends ? 2 : 0, nullptr);
     for (auto &ev : sl.events) {
@@ -628,12 +722,16 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         return r;
     };
     if (e == hipSuccess && ends) { what = "event node"; e = add_event(sl.events[0]); }
-    // all steps in one launch; the last step's sums go to the bound edge-sum
-    // buffer (later eager emits read it); edges go to the bound outputs
+    // all steps and their edges in one launch; the last step's sums go to the
+    // bound edge-sum buffer (later eager emits read it)
+    if (!per_step) {
+        ro.eidx_mid = (int32_t *)h->edge_scratch;
+        ro.eattr_mid = (float *)(ro.eidx_mid + 2 * h->sz.edge_capacity);
+    }
     p.actions = actions;
     p.ro = ro;
-    p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, 0, sl.gran + 2, h->roll_status,
-                                  (uint32_t *)sl.gran};
+    p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, xW, xNG, 0, sl.gran + 2,
+                                  h->roll_status, (uint32_t *)sl.gran};
     if (e == hipSuccess) {
         what = "rollout kernel node";
         hipKernelNodeParams kp = {};
@@ -647,22 +745,14 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         hipGraphNode_t n;
         e = hipGraphAddKernelNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0, &kp);
         if (e == hipSuccess) prev = n;
+        sl.direct = !ends;
+        sl.fn = roll_fn;
+        sl.grid = kp.gridDim;
+        sl.block = kp.blockDim;
+        sl.lds = kp.sharedMemBytes;
+        sl.args = p;
     }
     if (e == hipSuccess && ends) { what = "event node"; e = add_event(sl.events[1]); }
-    if (e == hipSuccess) {   // the last step's edges (see gsm_roll_seg_kernel)
-        what = "emit kernel node";
-        hipKernelNodeParams kp = {};
-        void *args[] = {&p};
-        kp.func = const_cast<void *>(gsm::emit_kernel_fn(p));
-        kp.gridDim = dim3(gsm::grid_blocks(p));
-        kp.blockDim = dim3(gsm::block_threads(p));
-        kp.sharedMemBytes = (unsigned)gsm::emit_kernel_lds(p);
-        kp.kernelParams = args;
-        kp.extra = nullptr;
-        hipGraphNode_t n;
-        e = hipGraphAddKernelNode(&n, sl.graph, prev ? &prev : nullptr, prev ? 1 : 0, &kp);
-        if (e == hipSuccess) prev = n;
-    }
     if (e != hipSuccess) {
         drop_slot(sl);
         char where[96];
@@ -698,7 +788,7 @@ int gsm_graph_roll_status(gsm_handle *h, int32_t *gave_up) {
     if (!h->roll_status) return GSM_OK;
     uint32_t v = 0;
     hipError_t e = hipMemcpy(&v, h->roll_status, sizeof v, hipMemcpyDeviceToHost);
-    if (e == hipSuccess && v) e = hipMemset(h->roll_status, 0, 16);
+    if (e == hipSuccess && v) e = clear_status(h);
     if (e != hipSuccess) return hip_fail(h, e, "rollout status read");
     *gave_up = v ? 1 : 0;
     return GSM_OK;
@@ -752,11 +842,17 @@ static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_
     sl.kern = kern;
     e = hipGraphCreate(&sl.graph, 0);
     if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "hipGraphCreate"); }
+    if (lag && !h->roll_status) {   // the ragged lagged step's bounded wait reports through it
+        e = hipMalloc(&h->roll_status, 16);
+        if (e == hipSuccess) e = clear_status(h);
+        if (e != hipSuccess) { h->roll_status = nullptr; drop_slot(sl); return hip_fail(h, e, "hipMalloc (status)"); }
+    }
     gsm::DevParams p = h->dp;
     p.mode = GSM_MODE_STEP;
     p.action_fmt = action_fmt;
     p.env_mask = nullptr;
     p.reseed = 0;
+    if (lag) p.roll.status = h->roll_status;
     hipGraphNode_t prev = nullptr;
     const char *what = "";
     int at = 0;
@@ -839,8 +935,15 @@ static int capture_impl(gsm_handle *h, int32_t slot, const void *actions, int64_
 int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream) {
     if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
     if (bad_slot(slot)) return fail(h, GSM_EINVAL, "bad graph slot");
-    if (!h->slots[slot].exec) return fail(h, GSM_ESTATE, "no graph captured in this slot");
-    const hipError_t e = hipGraphLaunch(h->slots[slot].exec, as_stream(stream));
+    gsm_handle::Slot &sl = h->slots[slot];
+    if (!sl.exec) return fail(h, GSM_ESTATE, "no graph captured in this slot");
+    if (sl.direct) {
+        void *args[] = {&sl.args};
+        const hipError_t e = hipLaunchKernel(sl.fn, sl.grid, sl.block, args, sl.lds, as_stream(stream));
+        if (e != hipSuccess) return hip_fail(h, e, "hipLaunchKernel (rollout)");
+        return GSM_OK;
+    }
+    const hipError_t e = hipGraphLaunch(sl.exec, as_stream(stream));
     if (e != hipSuccess) return hip_fail(h, e, "hipGraphLaunch");
     return GSM_OK;
 }
@@ -930,6 +1033,7 @@ int gsm_destroy(gsm_handle *h) {
     if (h->cap_stream) (void)hipStreamDestroy(h->cap_stream);
     if (h->bsum_alt) (void)hipFree(h->bsum_alt);
     if (h->roll_status) (void)hipFree(h->roll_status);
+    if (h->edge_scratch) (void)hipFree(h->edge_scratch);
     if (h->order_copied) (void)hipEventSynchronize(h->order_copied);
     if (h->block_order) (void)hipFree(h->block_order);
     if (h->order_host) (void)hipHostFree(h->order_host);

@@ -9,10 +9,7 @@ constexpr int kWave = 64;
 constexpr int kWavesPerBlock = 4;              // one env per wave
 constexpr int kBlock = kWave * kWavesPerBlock;
 enum : int32_t { kPathSeg = 1, kPathRagged = 2, kPathTile = 3 };
-#ifndef GSM_TILE_BLOCK
-#define GSM_TILE_BLOCK 512
-#endif
-constexpr int kTileBlock = GSM_TILE_BLOCK;     // tile path: one workgroup per env
+constexpr int kTileBlock = 512;                // tile path: one workgroup per env
 enum : int32_t { kScnNav = 0, kScnPolygon = 1, kScnLine = 2, kScnMixed = 3 };
 constexpr int kTileEmitScr = 6144;   // tile emitter: staged edge words per env (24 KB of LDS)
 constexpr int kRaggedMaxAgents = 32;                                  // = GSM_RAGGED_MAX_AGENTS
@@ -24,10 +21,11 @@ __host__ __device__ constexpr int lsa_cost_bytes(int nmax) { return 4 * ((nmax +
 __host__ __device__ constexpr int lsa_lds_bytes(int nmax) {
     return ((lsa_cost_bytes(nmax) + 15) & ~15) + 16 * kRaggedMaxAgents + 4 * kRaggedMaxAgents;
 }
-#ifndef GSM_SEG_GMAX   // cap on envs per wave (C2, 3 x 4096: G = 4 runs 6.0 us per step against 6.9 at G = 10)
-#define GSM_SEG_GMAX 4
-#endif
-constexpr int kMaxSegEnvsPerWave = GSM_SEG_GMAX;   // keeps a block's envs (4G) within one wave's lanes
+// cap on envs per wave, keeping a block's envs (4G) within one wave's lanes
+// (C2, 3 x 4096: G = 4 runs 6.0 us per step against 6.9 at G = 10)
+constexpr int kMaxSegEnvsPerWave = 4;
+// steps of a one-env-per-wave rollout launch (12-bit granule tags, gsm_device.h Xfer)
+constexpr int kXferMaxSteps = 4095;
 
 // Everything a launch needs, passed by value (kernarg segment, < 4 KB).
 // fp32 constants are formed on the host exactly as oracle/batch_ref.py:Spec
@@ -86,28 +84,38 @@ struct DevParams {
         float *edge_attr;
         int64_t cap;
     } lag;
-    // Fused rollout (segmented path, one env per wave, graph chains): K
-    // consecutive steps in one launch (gsm_roll_seg_kernel). Iteration k runs
-    // step t_first + k with the actions at actions + ((t_first + k) %
-    // n_actions) * stride and emits the previous step's edges into p.lag's
-    // outputs; the CSR prefix of step t crosses workgroups through `gran`
-    // (8-byte {tag, workgroup edge sum} granules, aggregates [K][grid] then
-    // inclusive prefixes [K][grid]; tag = epoch << 16 | (k + 1), the launch
-    // epoch read from `*epoch` at launch start and advanced by the emit launch
-    // that ends the graph, so no granule is ever cleared between launches).
-    // `status` is set when a bounded wait gave up.
+    // Fused rollout (one env per wave or per workgroup, graph chains): K
+    // consecutive steps in one launch (gsm_roll_seg_kernel,
+    // gsm_roll_tile_kernel). Iteration k runs step t_first + k with the
+    // actions at actions + ((t_first + k) % n_actions) * stride and emits the
+    // edges of an earlier step (ro); the tail after the loop emits the last.
+    // The CSR prefix of step t crosses waves / workgroups through `gran`,
+    // after a 16-byte header holding the launch epoch: one-env-per-wave
+    // rollouts use 32-bit per-wave granules and group sums (gsm_device.h Xfer,
+    // emission two steps behind); the tile rollout 8-byte {tag, env edge sum}
+    // granules, aggregates [K][grid] then inclusive prefixes [K][grid]
+    // (decoupled look-back, tag = epoch << 16 | (k + 1)). The epoch is
+    // advanced by the launch's last wave / workgroup once every one has read
+    // it, so no granule is ever cleared between launches. `status` is set when
+    // a bounded wait gave up.
     struct Roll {
         const char *actions;
         int64_t stride;
-        int32_t n_actions, t_first, K, pad;
+        int32_t n_actions, t_first, K;
+        int32_t xW, xNG;      // one-env-per-wave rollouts: waves of the grid, groups of 64 (gsm_device.h Xfer)
+        int32_t pad;
         uint64_t *gran;
         uint32_t *status;
-        uint32_t *epoch;      // nullptr outside rollout graphs (the emit kernel then leaves it)
+        uint32_t *epoch;
     } roll;
     // A rollout's per-step outputs: step k's at base + k * stride (elements;
     // stride 0 = every step into the bound buffers, > 0 = a rollout buffer's
     // slots, gsm_graph_capture_into). Edges of step k at index / attr + k *
-    // e_s, edge_ptr + k * ep_s, capacity cap.
+    // e_s, edge_ptr + k * ep_s, capacity cap. In the bound buffers (stride 0)
+    // only the last step's edges go to eidx / eattr; the earlier steps' go to
+    // the library's scratch eidx_mid / eattr_mid (same capacity): workgroups
+    // emit at different paces, and an earlier step's edges written late must
+    // not land on the last step's (roll_edge_sink).
     struct RollOut {
         float *nf, *rew, *cost;
         uint8_t *done;
@@ -116,6 +124,8 @@ struct DevParams {
         int32_t *eidx;
         float *eattr;
         int64_t nf_s, rc_s, done_s, ec_s, ep_s, ei_s, ea_s, cap;
+        int32_t *eidx_mid;
+        float *eattr_mid;
     } ro;
 };
 
@@ -125,6 +135,16 @@ struct EdgeSink {
     float *attr;
     int64_t cap;
 };
+
+// Where a rollout launch of K steps emits step j's edges (DevParams::RollOut):
+// a rollout buffer's slot j, else the bound buffers for the last step and the
+// library's scratch for the others.
+template <bool kSlots, typename Params>
+__device__ __forceinline__ EdgeSink roll_edge_sink(const Params &q, int j, int K) {
+    if (kSlots) return EdgeSink{q.ro.eidx + j * q.ro.ei_s, q.ro.eattr + j * q.ro.ea_s, q.ro.cap};
+    if (j == K - 1) return EdgeSink{q.ro.eidx, q.ro.eattr, q.ro.cap};
+    return EdgeSink{q.ro.eidx_mid, q.ro.eattr_mid, q.ro.cap};
+}
 
 // Launch the step kernel (physics / reset / observe by p.mode) and the edge
 // emitter for all B envs on `s`. Returns the first hipError_t.
@@ -159,6 +179,8 @@ hipError_t upload_ragged_tables();
 size_t step_kernel_lds(const DevParams &p);
 size_t emit_kernel_lds(const DevParams &p);
 hipError_t launch_step_kernel(const DevParams &p, hipStream_t s);
+// rollout granules: word 0 = epoch0, the rest 0, by agent-scope atomic stores
+hipError_t launch_granule_init(void *g, size_t bytes, uint32_t epoch0, hipStream_t s);
 hipError_t launch_emit_kernel(const DevParams &p, hipStream_t s);
 hipError_t launch_attn_aggregate(const float *q, const float *k, const float *v, const float *edge_w,
                                  const float *w_e, const int64_t *row_ptr, const int32_t *col,

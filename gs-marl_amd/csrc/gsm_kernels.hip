@@ -46,16 +46,13 @@ const void *emit_kernel_fn(const DevParams &p) {
     if (p.path == kPathTile) return emit_tile_kernel_fn();
     return emit_seg_kernel_fn(p);
 }
-#ifndef GSM_LDS_PAD   // experiment: extra LDS per segmented step workgroup (caps residency)
-#define GSM_LDS_PAD 0
-#endif
 size_t step_kernel_lds(const DevParams &p) {
     // segmented / ragged: + per-wave edge sums and (lagged emission) per-wave prefix words;
     // ragged: + the lagged emission's staged inputs (gsm_ragged_kernels.hip RaggedLagLds:
     // counters, 4 x 64 row masks, 4 x E_max positions)
     if (p.path == kPathTile) return (size_t)p.wave_lds_step;
     const size_t lag = p.path == kPathRagged ? 64 + 8 * kWave * kWavesPerBlock + 8 * (size_t)kWavesPerBlock * p.E : 0;
-    return (size_t)kWavesPerBlock * p.wave_lds_step + 32 + lag + GSM_LDS_PAD;
+    return (size_t)kWavesPerBlock * p.wave_lds_step + 32 + lag;
 }
 size_t emit_kernel_lds(const DevParams &p) {
     return p.path == kPathTile ? (size_t)p.wave_lds_emit : (size_t)kWavesPerBlock * p.wave_lds_emit + 16;
@@ -80,6 +77,26 @@ hipError_t launch_step(const DevParams &p, hipStream_t s) {
     hipError_t e = launch_step_kernel(p, s);
     if (e != hipSuccess) return e;
     return launch_emit_kernel(p, s);
+}
+
+// Rollout granules are initialised by the same agent-scope stores the
+// rollouts publish with: a recycled allocation can otherwise show an agent-scope
+// load the previous allocation's granules (observed: a memset's zeros did not
+// supersede them), and a stale granule whose tag happens to match would be
+// taken for this launch's. Word 0 is the launch epoch, the rest zero.
+__global__ __launch_bounds__(256) void gsm_granule_init_kernel(uint32_t *g, int64_t words, uint32_t epoch0) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < words; i += (int64_t)gridDim.x * blockDim.x)
+        __hip_atomic_store((gu32 *)(g + i), i == 0 ? epoch0 : 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+hipError_t launch_granule_init(void *g, size_t bytes, uint32_t epoch0, hipStream_t s) {
+    const int64_t words = (int64_t)(bytes / 4);
+    const int64_t need = (words + 255) / 256;
+    const int blocks = (int)(need < 1024 ? need : 1024);
+    uint32_t *gp = (uint32_t *)g;
+    int64_t n = words;
+    void *args[] = {&gp, &n, &epoch0};
+    return hipLaunchKernel(reinterpret_cast<const void *>(&gsm_granule_init_kernel), dim3(blocks), dim3(256), args, 0,
+                           s);
 }
 
 }  // namespace gsm

@@ -225,10 +225,6 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
         *own = __builtin_nanf("");
         return -1;
     }
-#ifdef GSM_ABL_NO_LSA   // timing-only ablation: identity assignment
-    *own = 0.0f;
-    return col ? lane : -1;
-#endif
     // column `lane` of C held in registers, C[i][lane] picked by the
     // wave-uniform row i (s_set_gpr_idx): no LDS round trip in the path loop;
     // the LDS copy serves the row-parallel passes and the final cost lookup.
@@ -524,12 +520,19 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
         }
     }
     if (!solved) {
+        // The cold recurrence is normally the tail of its launch (an env whose
+        // warm start could not be certified: exact float32 ties).
+        // It runs at raised wave priority so that, until the other waves of
+        // its SIMD finish, its dependent chain is issued first (priority only
+        // orders issue: results are unchanged; C4 -0.9% per step).
+        __builtin_amdgcn_s_setprio(3);
         u = 0.0;
         v = 0.0;
         col4row = -1;
         row4col = -1;
         for (int cur = 0; cur < N; ++cur)
             if (!augment(cur)) break;
+        __builtin_amdgcn_s_setprio(0);
     }
     if (w.v && col) {
         w.v[lane] = v;
@@ -673,16 +676,10 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
         float own;
         int nit = 0;
         GSM_STAMP(p, b, 0);
-#ifdef GSM_RAGGED_PRIO   // experiment: the assignment's long dependent chain at raised priority
-        if (s.N >= GSM_RAGGED_PRIO) __builtin_amdgcn_s_setprio(3);
-#endif
 #ifdef GSM_STAMPS
         sigma = wave_lsa(s.N, lane, cp, slot, s_lsa, &own, lsa_warm, &nit, p.stamps ? p.stamps + (int64_t)b * 16 + 4 : nullptr);
 #else
         sigma = wave_lsa(s.N, lane, cp, slot, s_lsa, &own, lsa_warm, &nit);
-#endif
-#ifdef GSM_RAGGED_PRIO
-        __builtin_amdgcn_s_setprio(0);
 #endif
         GSM_STAMP(p, b, 1);
 #ifdef GSM_STAMPS
@@ -791,11 +788,6 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
     return edges;
 }
 
-#ifdef GSM_RAGGED_OCC   // experiment: waves per SIMD
-#define GSM_RAGGED_ATTR __attribute__((amdgpu_waves_per_eu(GSM_RAGGED_OCC)))
-#else
-#define GSM_RAGGED_ATTR
-#endif
 __device__ void ragged_env_emit_rows(const DevParams &p, const int b, const int lane, const int64_t off,
                                      const float2 *s_pos, const RShape &s, uint64_t mask, const EdgeSink &out);
 
@@ -830,7 +822,7 @@ __device__ __forceinline__ RaggedLagLds ragged_lag_lds(unsigned char *base, int 
 }
 
 template <bool kLag>
-__global__ __launch_bounds__(kBlock) GSM_RAGGED_ATTR void gsm_step_ragged_kernel(DevParams p) {
+__global__ __launch_bounds__(kBlock) void gsm_step_ragged_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;   // wave-uniform: env shape, loops and assignment state stay scalar
     // env block of this workgroup (mixed: heaviest first, gsm_abi.hip update_block_order)
@@ -884,11 +876,18 @@ __global__ __launch_bounds__(kBlock) GSM_RAGGED_ATTR void gsm_step_ragged_kernel
         j = __builtin_amdgcn_readfirstlane(j);
         if (j < nlive) {
             // every wave's inputs staged (set early in every wave's step;
-            // bounded wait)
-            for (int spin = 0; spin < (1 << 20); ++spin) {
+            // bounded wait: should it ever run out, nothing is emitted from
+            // unstaged LDS and the sticky status word says so)
+            bool staged = false;
+            for (int spin = 0; spin < (1 << 20) && !staged; ++spin) {
                 const int r = lane < nlive ? __hip_atomic_load(&L.ready[lane], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) : 1;
-                if (__all(r != 0)) break;
-                __builtin_amdgcn_s_sleep(2);
+                staged = __all(r != 0);
+                if (!staged) __builtin_amdgcn_s_sleep(2);
+            }
+            if (!staged) {
+                if (lane == 0 && p.roll.status)
+                    __hip_atomic_store((gu32 *)p.roll.status, 3u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                j = nlive;
             }
             // exclusive prefix of the preceding workgroups' previous sums
             int acc = 0;

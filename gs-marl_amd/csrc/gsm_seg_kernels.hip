@@ -611,27 +611,17 @@ __device__ __forceinline__ void block_emit(const DevParams &p, const Shape<kN, k
     const int first = blockIdx.x * kWavesPerBlock * s.G;
     // one env per wave, compile-time shape: the env's list is staged in LDS
     // before the prefix exchange (needs only local counts)
-#ifdef GSM_ABL_NOSTAGE   // timing experiment: per-lane row writes only
-    constexpr bool kStaged = false;
-#else
     constexpr bool kStaged = kG == 1 && kN > 0 && kN <= 31 && kNo <= 32;
-#endif
     int staged = -1;
-#ifndef GSM_ABL_NO_ROWS
     if constexpr (kStaged) {
         if (L.b < p.B) staged = stage_rows<kN, kNo>(L, s_scr, scr_cap, mask);
     }
-#endif
     const int acc = wave_total(pre.acc);
     const int incl_k = wave_scan(pre.cnt_k);     // envs of this block in order
-#ifdef GSM_ABL_NO_LAGBAR   // timing-only: no workgroup exchange of the prefix
-    int64_t base = acc;
-#else
     if (L.lane == 0) s_red[L.wave] = acc;
     __syncthreads();
     int64_t base = 0;
     for (int q = 0; q < kWavesPerBlock; ++q) base += s_red[q];
-#endif
     int my_cnt, before;
     if constexpr (kG == 1) {
         my_cnt = __builtin_amdgcn_readlane(pre.cnt_k, L.wave);
@@ -646,31 +636,19 @@ __device__ __forceinline__ void block_emit(const DevParams &p, const Shape<kN, k
         edge_ptr[L.b] = env_off;
         if (L.b == p.B - 1) edge_ptr[p.B] = env_off + my_cnt;
     }
-#ifdef GSM_ABL_NO_ROWS   // timing-only ablation (no edges written)
-    if (my_cnt < 0)
-#endif
-    {
-        if constexpr (kStaged) {
-            // wave-uniform: the staged path when the env's list fit the scratch
-            // and fits the outputs (a redirected slot may be smaller than the
-            // worst case)
-            if (staged >= 0 && env_off + staged <= out.cap) {
-                write_staged<kN, kNo>(L, s_pos, s_scr, staged, env_off, out);
-                return;
-            }
+    if constexpr (kStaged) {
+        // wave-uniform: the staged path when the env's list fit the scratch
+        // and fits the outputs (a redirected slot may be smaller than the
+        // worst case)
+        if (staged >= 0 && env_off + staged <= out.cap) {
+            write_staged<kN, kNo>(L, s_pos, s_scr, staged, env_off, out);
+            return;
         }
-        emit_rows<kN, kNo, kG>(s, L, s_pos, mask, env_off, out, env_off + my_cnt > out.cap);
     }
+    emit_rows<kN, kNo, kG>(s, L, s_pos, mask, env_off, out, env_off + my_cnt > out.cap);
 }
 
 // ---------------------------------------------------------------------------
-#ifdef GSM_STEP_SGPR   // experiment: SGPR budget (residency = floor(800 / (ceil(sgpr/16)*16 + 16)) waves/SIMD)
-#define GSM_STEP_ATTR __attribute__((amdgpu_num_sgpr(GSM_STEP_SGPR)))
-#elif defined(GSM_STEP_OCC)   // experiment: ask for GSM_STEP_OCC waves per SIMD
-#define GSM_STEP_ATTR __attribute__((amdgpu_waves_per_eu(GSM_STEP_OCC)))
-#else
-#define GSM_STEP_ATTR
-#endif
 // Global inputs of one env for a one-env-per-wave (G = 1) wave, loaded into
 // registers before the first wait. (Processing two envs per wave in turn with
 // the second's loads in flight measured slower: DESIGN.md §8.)
@@ -834,9 +812,6 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
             const float2 pi = s_pos[m];
             float Fx = u.x, Fy = u.y;
             uint64_t cm = cand_prev;
-#ifdef GSM_ABL_NO_CONTACT   // timing-only
-            cm = 0;
-#endif
             while (cm) {
                 const int c = __builtin_ctzll(cm);
                 cm &= cm - 1;
@@ -881,12 +856,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
     uint64_t row, cand;
     int ccnt;
     bool coinc;
-#ifdef GSM_ABL_NO_SWEEP   // timing-only
-    row = oo; cand = 0; ccnt = 0; coinc = false;
-    asm volatile("" :: "v"(pm.x), "v"(pm.y));
-#else
     obs_sweep<kN, kNo, kG>(p, s, L, s_pos, s_nf, pm, full, oo, row, cand, ccnt, coinc);
-#endif
     GSM_STAMP(p, wid, 4);
 
     // reward / cost callbacks
@@ -975,18 +945,11 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
             const int len = (full_rows ? E : N) * 7;
             float *dst = q.node_feat + (int64_t)(b0 + g) * E * 7;
             const float *src = s_nf + g * E * 7;
-#ifdef GSM_ABL_NO_NF   // timing-only
-            if (len > 0) continue;
-#endif
             for (int q = L.lane; q < len; q += kWave) dst[(uint32_t)q] = src[q];
         }
     }
 
     GSM_STAMP(p, wid, 6);
-#ifdef GSM_ABL_FUSED_PADDED   // timing-only: emit here at a fixed per-env stride
-    emit_rows<kN, kNo, kG>(s, L, s_pos, row, (int64_t)(L.live ? L.b : 0) * (p.edge_capacity / p.B),
-                           EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity});
-#endif
     // App. A S16 flags of the final state: a coincident pair (from the sweep),
     // an agent at a non-finite position
     uint8_t deg = 0;
@@ -1025,7 +988,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
 }
 
 template <int kN, int kNo, int kFmt, bool kLag>
-__global__ __launch_bounds__(kBlock) GSM_STEP_ATTR void gsm_step_seg_kernel(DevParams p) {
+__global__ __launch_bounds__(kBlock) void gsm_step_seg_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Shape<kN, kNo> s(p);
     constexpr int kG = envs_per_wave<kN, kNo>();
@@ -1099,9 +1062,6 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
     block_emit<kN, kNo, kG>(p, s, L, s_pos, mask, pre, s_red, p.edge_ptr,
                             EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity}, (uint32_t *)(s_pos + E),
                             (p.wave_lds_emit - 8 * G * E) / 4);
-    // the emit launch that ends a rollout graph advances the graph's granule
-    // epoch (the rollout launch has completed; the next one reads it)
-    if (p.roll.epoch && blockIdx.x == 0 && threadIdx.x == 0) *p.roll.epoch = (*p.roll.epoch + 1u) & 0xffffu;
     GSM_STAMP(p, wid, 4);
     GSM_RSTAMP(p, wid, 9);
 }
@@ -1117,24 +1077,24 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
 // Iteration k (step t = t_first + k): physics, observation sweep, reward /
 // cost, auto-reset and every store of step t exactly as gsm_step_seg_kernel
 // (same operations in the same order: bit-identical outputs); the
-// workgroup's edge sum of step t is published as an 8-byte {tag = k + 1, sum}
-// granule (one relaxed agent-scope store: write-through, no fence); then the
-// edges of step t - 1 are emitted from the positions and row masks kept from
-// the previous iteration, at the CSR offset = the sum of the preceding
-// workgroups' granules of iteration k - 1 (relaxed agent-scope loads, every
-// tag checked). Those granules were published one iteration earlier, so the
-// wait is normally already satisfied. A workgroup waits only on workgroups
-// with smaller index (dispatched before it), so the chain always progresses;
-// every wait is bounded (kRollSpinTicks, then p.roll.status is set and the
-// launch drains). The state the launch starts from had its edges emitted by
-// whatever ran before. The last step's edges are left to an emit launch: in
-// the shared output buffers they must land after every workgroup's emission of
-// the earlier steps (a workgroup may trail its successors by several steps),
-// which a kernel boundary orders for ~1.5 us where a grid barrier over 2048
-// workgroups would cost ~10 us (MI355X_MICROARCH.md price list).
-#ifndef GSM_ROLL_ATTR   // all 8 waves per SIMD resident (2048 workgroups at 8192 envs: one residency round)
+// workgroup's edge sum of step t is published as an 8-byte {tag, sum}
+// granule (tag = epoch << 16 | (k + 1); one relaxed agent-scope store:
+// write-through, no fence); then the edges of step t - 1 are emitted from the
+// positions and row masks kept from the previous iteration, at the CSR offset
+// found by a decoupled look-back over the preceding workgroups' granules
+// (relaxed agent-scope loads, every tag checked). Aggregates were published
+// one iteration earlier, so the walk normally never waits. A workgroup waits
+// only on workgroups with smaller index (dispatched before it), so the chain
+// always progresses; every wait is bounded (kRollSpinTicks, then
+// p.roll.status is set and the launch drains). A tail after the loop emits the
+// last step's edges; the last workgroup then advances the launch epoch. In
+// the bound buffers the earlier steps' edges go to a library scratch: a
+// workgroup may trail its successors by several steps, so only the last
+// step's edges may land in the shared outputs. (A barrier-free variant with
+// per-wave granules and emission two steps behind, gsm_device.h Xfer,
+// measured slower here: 9.95 vs 9.40 µs per step)
+// all 8 waves per SIMD resident (2048 workgroups at 8192 envs: one residency round)
 #define GSM_ROLL_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
-#endif
 // a lane's action of the given step row, as loaded (decoded by roll_force)
 template <int kN, int kFmt, typename Params>   // DevParams or its kernarg view
 __device__ __forceinline__ float4 roll_action_load(const Params &p, int row, int64_t eb, uint32_t ma) {
@@ -1216,6 +1176,62 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     const uint32_t etag = *p.roll.epoch << 16;              // this launch's tag base
     int arow = p.roll.t_first % n_act;                      // action row of the current step
     uint8_t deg = 0;                                        // App. A S16 flags of the final state
+    // The edges of step t_first + k - 1, emitted in iteration k (k = 1..K-1)
+    // and by the tail after the loop (k = K): kept positions and row masks;
+    // the counts of this workgroup's envs are read before the exchange barrier.
+    auto emit_prev = [&](const int k, const Lane &L) {
+        const int par = k & 1;
+        const int *cb = s_bc + (1 - par) * kWavesPerBlock;   // this workgroup's counts of step t - 1
+        // the env's list staged first (needs only its own row counts)
+        const int staged = wave_live ? stage_rows<kN, kNo>(L, (uint32_t *)s_nf, scr_cap, oo) : -1;
+        // wave 0 walks back over the predecessors, hands the workgroup's
+        // offset to the other waves and publishes its inclusive prefix
+        if (wave == 0) {
+            KernargParams &qe = late_params();
+            const int64_t kb = (int64_t)(k - 1) * gridDim.x;
+            const int ex = roll_lookback(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
+                                         etag | (uint32_t)k, qe.roll.status, L.lane);
+            if (L.lane == 0) {
+                s_red[0] = ex;
+                __hip_atomic_store((gu64 *)(qe.roll.gran + (int64_t)K * gridDim.x + kb + blockIdx.x),
+                                   ((uint64_t)(etag | (uint32_t)k) << 32) |
+                                       (uint32_t)(ex + cb[0] + cb[1] + cb[2] + cb[3]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // After the tail's look-back of the LAST workgroup every
+                // workgroup has published a granule of this launch, so all
+                // have read the epoch: advance it for the next launch
+                // (granules are never cleared; a stale one cannot match).
+                if (k == K && blockIdx.x == gridDim.x - 1)
+                    __hip_atomic_store((gu32 *)qe.roll.epoch, ((etag >> 16) + 1u) & 0xffffu, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        int before = 0;
+        for (int w = 0; w < kWavesPerBlock; ++w) before += w < wave ? cb[w] : 0;
+        const int my_cnt = cb[wave];
+        int64_t env_off = (int64_t)s_red[0] + before;
+        // (an offset past the capacity is a legal overflow of a small slot:
+        // edge_ptr keeps it, the writes below stop at the capacity)
+        if (env_off < 0) {   // a broken hand-off: never write out of bounds
+            if (L.lane == 0) __hip_atomic_store((gu32 *)p.roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            env_off = p.ro.cap;
+        }
+        if (wave_live) {
+            KernargParams &qs = late_params();
+            if (L.lane == 0) {
+                int64_t *const eptr = qs.ro.eptr + (kSlots ? (k - 1) * qs.ro.ep_s : 0);
+                eptr[L.b] = env_off;
+                if (L.b == p.B - 1) eptr[p.B] = env_off + my_cnt;
+            }
+            const EdgeSink out = roll_edge_sink<kSlots>(qs, k - 1, K);
+            if (staged >= 0 && env_off + staged <= out.cap)
+                write_staged<kN, kNo>(L, s_prev, (uint32_t *)s_nf, staged, env_off, out);
+            else
+                emit_rows<kN, kNo, 1>(s, L, s_prev, oo, env_off, out, env_off + my_cnt > out.cap);
+        }
+        wave_sync();
+    };
     for (int k = 0; k < K; ++k) {
         // lane-derived values re-formed every iteration (an asm barrier): held
         // across the loop they would pin their hoisted addresses in VGPRs
@@ -1389,60 +1405,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
                 }
             }
         }
-        // the edges of step t - 1 (kept positions and row masks; the counts of
-        // this workgroup's envs are read before the exchange barrier)
-#ifndef ROLLX_NOEMIT
-        if (k > 0) {
-            const int *cb = s_bc + (1 - par) * kWavesPerBlock;   // this workgroup's counts of step t - 1
-            // the env's list staged first (needs only its own row counts)
-            const int staged = wave_live ? stage_rows<kN, kNo>(L, (uint32_t *)s_nf, scr_cap, oo) : -1;
-            // wave 0 walks back over the predecessors, hands the workgroup's
-            // offset to the other waves and publishes its inclusive prefix
-            if (wave == 0) {
-                KernargParams &qe = late_params();
-                const int64_t kb = (int64_t)(k - 1) * gridDim.x;
-#ifdef ROLLX_NOPRE
-                const int ex = 0;
-#else
-                const int ex = roll_lookback(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
-                                             etag | (uint32_t)k, qe.roll.status, L.lane);
-#endif
-                if (L.lane == 0) {
-                    s_red[0] = ex;
-                    __hip_atomic_store((gu64 *)(qe.roll.gran + (int64_t)K * gridDim.x + kb + blockIdx.x),
-                                       ((uint64_t)(etag | (uint32_t)k) << 32) |
-                                           (uint32_t)(ex + cb[0] + cb[1] + cb[2] + cb[3]),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            __syncthreads();
-            int before = 0;
-            for (int w = 0; w < kWavesPerBlock; ++w) before += w < wave ? cb[w] : 0;
-            const int my_cnt = cb[wave];
-            int64_t env_off = (int64_t)s_red[0] + before;
-            // (an offset past the capacity is a legal overflow of a small slot:
-            // edge_ptr keeps it, the writes below stop at the capacity)
-            if (env_off < 0) {   // a broken hand-off: never write out of bounds
-                if (L.lane == 0) __hip_atomic_store((gu32 *)p.roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                env_off = p.ro.cap;
-            }
-            if (wave_live) {
-                KernargParams &qs = late_params();
-                if (L.lane == 0) {
-                    int64_t *const eptr = qs.ro.eptr + (kSlots ? (k - 1) * qs.ro.ep_s : 0);
-                    eptr[L.b] = env_off;
-                    if (L.b == p.B - 1) eptr[p.B] = env_off + my_cnt;
-                }
-                const EdgeSink out{qs.ro.eidx + (kSlots ? (k - 1) * qs.ro.ei_s : 0),
-                                   qs.ro.eattr + (kSlots ? (k - 1) * qs.ro.ea_s : 0), qs.ro.cap};
-                if (staged >= 0 && env_off + staged <= out.cap)
-                    write_staged<kN, kNo>(L, s_prev, (uint32_t *)s_nf, staged, env_off, out);
-                else
-                    emit_rows<kN, kNo, 1>(s, L, s_prev, oo, env_off, out, env_off + my_cnt > out.cap);
-            }
-            wave_sync();
-        }
-#endif
+        if (k > 0) emit_prev(k, L);
         // keep step t for the next iteration's emission and sweep
         oo = row;
         cand_prev = L.agent ? cand : 0ull;
@@ -1453,6 +1416,11 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         u = roll_force<kFmt>(late_params(), anext, L.agent);
         arow = nrow;
         wave_sync();
+    }
+    {   // the tail: the last step's edges
+        Lane L = L0;
+        asm volatile("" : "+v"(L.lane), "+v"(L.m));
+        emit_prev(K, L);
     }
     // the final state (what the next launch or an eager step reads)
     KernargParams &q = late_params();
@@ -1478,7 +1446,9 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
 // collectives for 24 agents) and action formats; anything else runs the
 // runtime-shape instantiation.
 #define GSM_SEG_SHAPES(X) X(3, 3) X(24, 24)
-#define GSM_ROLL_SHAPES(X) X(3, 3) X(24, 24)
+// rollout shapes: BASELINE's (3, 24 agents) and the reference's zero-shot
+// navigation sizes 6 and 12 (readme.md:75)
+#define GSM_ROLL_SHAPES(X) X(3, 3) X(6, 6) X(12, 12) X(24, 24)
 
 template <bool LAG>
 static const void *pick_step_seg(const DevParams &p) {

@@ -349,11 +349,7 @@ __device__ __forceinline__ int obs_sweep_any(const DevParams &p, const float2 *s
 // in one residency round (the compiler's default, 106 SGPRs, allowed 7 waves
 // and three workgroups per CU). Fits without scratch (78 SGPRs, 58 VGPRs);
 // step kernel 23.4 -> 22.0 us at C3.
-#ifndef GSM_TILE_OCC7   // experiment: the compiler's default occupancy
 #define GSM_TILE_ATTR __attribute__((amdgpu_waves_per_eu(8)))
-#else
-#define GSM_TILE_ATTR
-#endif
 // ---------------------------------------------------------------------------
 // edge emitter
 // ---------------------------------------------------------------------------
@@ -610,13 +606,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
     }
 
     // observation sweep of the post-step state: masks, collision counts, pairs
-#ifndef GSM_ABL_NO_SWEEP
     int pairs = p.tile_sym ? obs_sweep_sym(p, s_pos, sym, s_cost, eb, p.mode == kModeStep && !relaid)
                            : obs_sweep_any(p, s_pos, s_cost, eb, p.mode == kModeStep && !relaid, s_deg);
-#else
-    int pairs = 0;
-    for (int i = tid; i < N; i += kTileBlock) s_cost[i] = 0;
-#endif
     // reward and cost callbacks, episode accounting. The workgroup sums of
     // reward, collisions, directed radius pairs and the non-finite flag share
     // one LDS exchange (an auto-reset, rare, re-sweeps and exchanges again).
@@ -688,9 +679,6 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
     // step (one thread per row), goal/obstacle rows only on layout change
     float *nf = p.node_feat + eb * E * 7;
     const bool full = p.mode != kModeStep || relaid || p.nf_full;
-#ifdef GSM_ABL_NO_NF
-    if (!full) goto skip_nf;
-#endif
     for (int i = tid; i < N; i += kTileBlock) {
         const float2 v = s_vel[i], a = s_pos[i], g = s_pos[N + i];
         float *row = nf + (int64_t)i * 7;
@@ -715,9 +703,6 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_step_tile_kernel
             row[6] = e < 2 * N ? 1.0f : 2.0f;
         }
     }
-#ifdef GSM_ABL_NO_NF
-skip_nf:
-#endif
     // state
     if (p.mode == kModeStep || do_reset) {
         const int ne = relaid ? E : N;
@@ -757,8 +742,6 @@ __global__ __launch_bounds__(kTileBlock) void gsm_emit_tile_kernel(DevParams p) 
     int64_t off;   // (emit_env's exchange barrier also publishes the staged positions)
     emit_env(p, EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity}, s_pos, p.row_mask + eb * p.M * p.W, before,
              &off, s_red, s_scr, scr_cap, (int32_t)(eb * E));
-    // the emit launch that ends a rollout graph advances its granule epoch
-    if (p.roll.epoch && b == 0 && tid == 0) *p.roll.epoch = (*p.roll.epoch + 1u) & 0xffffu;
     if (tid == 0) {
         p.edge_ptr[b] = off;
         if (b == p.B - 1) p.edge_ptr[p.B] = off + p.edge_count[b];
@@ -808,7 +791,7 @@ template <bool kSlots>   // per-step outputs at base + k * stride (a rollout buf
 __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int b = blockIdx.x;
-    const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+    const int tid = threadIdx.x;
     const int N = p.N, E = p.E, W = p.W, M = p.M;
     float2 *s_pos = (float2 *)smem;           // [E]
     float2 *s_vel = s_pos + E;                // [N]
@@ -851,7 +834,9 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     int prev_edges = 0, bad = 0;
     __syncthreads();
 
-    for (int k = 0; k < K; ++k) {
+    // iterations 0..K-1 run step k and emit step k-1; iteration K (the tail)
+    // only emits step K-1
+    for (int k = 0; k <= K; ++k) {
         // thread-derived values re-formed every iteration (an asm barrier): held
         // across the loop their hoisted addresses would pin VGPRs
         int tid = (int)threadIdx.x;
@@ -859,6 +844,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         const int wave = tid >> 6, lane = tid & 63;
         uint64_t *const rout = s_rm + (k & 1) * M * W;
         const uint64_t *const rkeep = s_rm + ((k + 1) & 1) * M * W;   // the previous step's masks
+        int edges = 0;
+        if (k < K) {
         bool relaid = false;
         auto relayout = [&]() {   // scenario.reset_world with the Philox layout
             ep = ep + 1;
@@ -1004,7 +991,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                 row[6] = e < 2 * N ? 1.0f : 2.0f;
             }
         }
-        const int edges = pairs + 2 * N;   // directed radius edges + agent<->goal
+        edges = pairs + 2 * N;   // directed radius edges + agent<->goal
         if (tid == 0) {
             KernargParams &q = late_params();
             q.ro.done[(kSlots ? k * q.ro.done_s : 0) + b] = done ? 1 : 0;
@@ -1013,6 +1000,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                                ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)edges, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
+        }   // k < K
         // the previous step's edges at the offset of the look-back
         if (k > 0) {
             int ex = 0;
@@ -1021,11 +1009,17 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                 KernargParams &q = late_params();
                 ex = roll_lookback(q.roll.gran + kb, q.roll.gran + (int64_t)K * gridDim.x + kb, etag | (uint32_t)k,
                                    q.roll.status, lane);
-                if (lane == 0)
+                if (lane == 0) {
                     __hip_atomic_store((gu64 *)(late_params().roll.gran + (int64_t)K * gridDim.x + kb + b),
                                        ((uint64_t)(etag | (uint32_t)k) << 32) | (uint32_t)(ex + prev_edges),
                                        __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
+                    // the tail's look-back of the last workgroup: every
+                    // workgroup has read the epoch (gsm_roll_seg_kernel)
+                    if (k == K && b == (int)gridDim.x - 1)
+                        __hip_atomic_store((gu32 *)q.roll.epoch, ((etag >> 16) + 1u) & 0xffffu, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                }
             }
             // (an offset past the capacity is a legal overflow of a small slot:
             // edge_ptr keeps it, emit_env stops its writes at the capacity)
@@ -1034,13 +1028,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                 ex = (int)min(p.ro.cap, (int64_t)0x7fffffff);
             }
             int64_t off;
-            {
-                KernargParams &q = late_params();
-                emit_env(p, EdgeSink{q.ro.eidx + (kSlots ? (k - 1) * q.ro.ei_s : 0),
-                                     q.ro.eattr + (kSlots ? (k - 1) * q.ro.ea_s : 0), q.ro.cap},
-                         s_prev, rkeep, tid == 0 ? ex : 0,
-                         &off, s_red, s_scr, kRollTileScr, g0);
-            }
+            emit_env(p, roll_edge_sink<kSlots>(late_params(), k - 1, K), s_prev, rkeep, tid == 0 ? ex : 0, &off,
+                     s_red, s_scr, kRollTileScr, g0);
             if (tid == 0) {
                 KernargParams &q = late_params();
                 int64_t *const eptr = q.ro.eptr + (kSlots ? (k - 1) * q.ro.ep_s : 0);
@@ -1048,11 +1037,13 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                 if (b == p.B - 1) eptr[p.B] = off + prev_edges;
             }
         }
-        __syncthreads();   // s_prev and the staged words read
-        for (int e = tid; e < E; e += kTileBlock) s_prev[e] = s_pos[e];
-        prev_edges = edges;
-        arow = arow + 1 == n_act ? 0 : arow + 1;
-        __syncthreads();
+        if (k < K) {
+            __syncthreads();   // s_prev and the staged words read
+            for (int e = tid; e < E; e += kTileBlock) s_prev[e] = s_pos[e];
+            prev_edges = edges;
+            arow = arow + 1 == n_act ? 0 : arow + 1;
+            __syncthreads();
+        }
     }
     // the final state (what the next launch or an eager step reads)
     for (int e = tid; e < E; e += kTileBlock) p.pos[eb * E + e] = s_pos[e];

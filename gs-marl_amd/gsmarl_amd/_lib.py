@@ -11,7 +11,7 @@ import os
 from pathlib import Path
 
 LIB_PATH = Path(os.environ.get("GSM_LIB_PATH") or Path(__file__).resolve().parent / "lib" / "libgsm.so")
-ABI_VERSION = 6
+ABI_VERSION = 7
 DEGENERATE_COINCIDENT, DEGENERATE_NONFINITE = 1, 2
 
 GSM_OK, GSM_EINVAL, GSM_EHIP, GSM_ESTATE = 0, -1, -2, -3
@@ -65,6 +65,13 @@ class GsmOutputs(C.Structure):
     _fields_ = [(n, C.c_void_p) for n in OUTPUT_FIELDS] + [("edge_capacity", C.c_int64)]
 
 
+STATE_FIELDS = ["pos", "vel", "step_count", "episode", "ep_acc", "ep_last", "env_shape"]
+
+
+class GsmState(C.Structure):
+    _fields_ = [(n, C.c_void_p) for n in STATE_FIELDS]
+
+
 # every symbol include/gsm.h declares, with its ctypes signature
 _P = C.c_void_p
 SIGNATURES = {
@@ -75,6 +82,8 @@ SIGNATURES = {
     "gsm_reset": (C.c_int, [_P, C.c_uint64, C.c_int, _P, _P]),
     "gsm_step": (C.c_int, [_P, _P, C.c_int, _P]),
     "gsm_observe": (C.c_int, [_P, _P]),
+    "gsm_get_state": (C.c_int, [_P, C.POINTER(GsmState), _P]),
+    "gsm_set_state": (C.c_int, [_P, C.POINTER(GsmState), _P]),
     "gsm_step_into": (C.c_int, [_P, _P, C.c_int, C.POINTER(GsmOutputs), _P]),
     "gsm_observe_into": (C.c_int, [_P, C.POINTER(GsmOutputs), _P]),
     "gsm_graph_capture_into": (C.c_int, [_P, C.c_int32, _P, C.c_int64, C.c_int32, C.c_int32, C.c_int,

@@ -240,17 +240,33 @@ class GpuBatchEnv:
         return render_frames(self.t["node_feat"], self.t["edge_ptr"], self.t["edge_index"], env_ids, width, height,
                              (c.agent_size, c.goal_size, c.obstacle_size), c.world_half or 0.0, edges)
 
+    def _state_keys(self):
+        return self.STATE_KEYS + (("env_shape",) if self.cfg.ragged else ())
+
     def get_state(self) -> dict:
-        return {k: self.t[k].clone() for k in self.STATE_KEYS}
+        """A copy of the simulator state (gsm_get_state): pos, vel, step_count,
+        episode, ep_acc, ep_last (+ env_shape for ragged batches)."""
+        out = {k: torch.empty_like(self.t[k]) for k in self._state_keys()}
+        st = _lib.GsmState(**{k: v.data_ptr() for k, v in out.items()})
+        self._chk(self.lib.gsm_get_state(self._h, C.byref(st), self._stream()), "gsm_get_state")
+        return out
 
     def set_state(self, state: dict, sync_edges: bool = True) -> dict:
-        """Overwrite state buffers and re-observe (which also refreshes the
-        derived per-position state the next step relies on)."""
+        """Overwrite state buffers and re-observe (gsm_set_state: the observe
+        also refreshes the derived per-position state the next step relies on).
+        Missing keys keep their current values."""
+        src = {}
         for k, v in state.items():
-            if k not in self.STATE_KEYS:
+            if k not in self._state_keys():
                 raise KeyError(k)
-            self.t[k].copy_(torch.as_tensor(v).to(self.t[k].dtype))
-        return self.observe(sync_edges)
+            t = torch.as_tensor(v).to(device=self.device, dtype=self.t[k].dtype).contiguous()
+            if t.shape != self.t[k].shape:
+                raise ValueError(f"state {k}: shape {tuple(t.shape)} != {tuple(self.t[k].shape)}")
+            src[k] = t
+        st = _lib.GsmState(**{k: v.data_ptr() for k, v in src.items()})
+        self._chk(self.lib.gsm_set_state(self._h, C.byref(st), self._stream()), "gsm_set_state")
+        self._state_src = src   # keep the sources alive until the stream has copied them
+        return self.outputs(sync_edges)
 
     # ------------------------------------------------------------ HIP graph
     def capture(self, actions_seq: Optional[torch.Tensor], n_steps: int, timing: bool = False,
@@ -261,9 +277,10 @@ class GpuBatchEnv:
         step), "unfused" (step + emit kernel per step), "step", "emit"
         (re-emits the current edges), "lag" (lagged step kernels only; the
         last step's edges are left unemitted — a timing tool) or "roll"
-        (steps 1..n_steps-1 in one fused rollout launch; one-env-per-wave
-        segmented configs only — GsmError otherwise; with time_ends the
-        events bracket that launch).
+        (all n_steps steps and their edges in ONE fused rollout launch;
+        navigation configs with a compiled rollout shape (3, 6, 12 or 24
+        agents with as many obstacles) or the tile path — GsmError otherwise;
+        with time_ends the events bracket that launch).
         timing: event nodes around every kernel (implies "unfused");
         time_ends: only around the whole graph (per-kernel means over
         back-to-back launches)."""
@@ -307,8 +324,9 @@ class GpuBatchEnv:
         return bool(fused.value)
 
     def roll_gave_up(self) -> bool:
-        """Whether a bounded wait of a fused rollout launch timed out since
-        the last call (outputs of that launch invalid); clears the flag."""
+        """Whether a bounded in-launch wait (a fused rollout launch, or the
+        ragged lagged chain's staging wait) timed out since the last call
+        (outputs of that launch invalid); clears the flag. Synchronises."""
         v = C.c_int32()
         self._chk(self.lib.gsm_graph_roll_status(self._h, C.byref(v)), "gsm_graph_roll_status")
         return bool(v.value)

@@ -125,15 +125,30 @@ class GraphRolloutBuffer:
         self._graph_actions = actions_seq
 
     def replay(self, slot: int = 0) -> None:
-        """Run a captured episode; slot 0 must already hold its first observation."""
+        """Run a captured episode; slot 0 must already hold its first observation.
+        The episode usually runs as one fused rollout launch, whose bounded
+        in-launch waits can (in principle) time out and leave invalid edges:
+        the next read of the buffer (``graph_batch``, ``validate``) checks."""
         self.env.replay(slot)
         n = self._graph_actions.shape[0]
         idx = torch.arange(self.T, device=self._graph_actions.device) % n
         self.actions.copy_(self._graph_actions[idx])
         self.step = self.T
+        self._unchecked = True
+
+    def validate(self) -> None:
+        """Raise if a replayed episode's launch gave up a bounded wait (its
+        CSR offsets and edges would be wrong). Synchronises; a no-op when no
+        replay happened since the last check."""
+        if getattr(self, "_unchecked", False):
+            self._unchecked = False
+            if self.env.roll_gave_up():
+                raise RuntimeError("GraphRolloutBuffer: a fused rollout launch gave up waiting on a "
+                                   "predecessor workgroup; the episode's edges are invalid")
 
     def after_update(self) -> None:
         """Carry the last observation into slot 0 for the next rollout."""
+        self.validate()
         for k in self.FIELDS + (("assign",) if self.ragged else ()):
             buf = getattr(self, k)
             buf[0].copy_(buf[self.step])
@@ -145,7 +160,9 @@ class GraphRolloutBuffer:
         [K*E, 7], edge_index [2, sum] int64 with local ids k*E + e, edge_attr,
         batch [K*E] (sample of each node), ptr [K+1] (edge offsets).
         Raises ValueError if a requested sample's edges were truncated because
-        its slot overflowed the per-slot edge capacity (``overflowed()``)."""
+        its slot overflowed the per-slot edge capacity (``overflowed()``), and
+        RuntimeError if the replayed episode's launch gave up a bounded wait."""
+        self.validate()
         E = self.E
         t = t_idx.to(self.edge_ptr.device, torch.int64)
         b = b_idx.to(self.edge_ptr.device, torch.int64)

@@ -35,8 +35,10 @@ extern "C" {
 /* 4: lagged-emission graph chains (GSM_GRAPH_UNFUSED / _LAG_ONLY), gsm_render
  * 5: degenerate-state handling: gsm_config.strict_degenerate,
  *    gsm_buffers.degenerate */
-/* 6: fused rollout graphs (GSM_GRAPH_ROLL, gsm_graph_roll_status, gsm_graph_info) */
-#define GSM_ABI_VERSION 6
+/* 6: fused rollout graphs (GSM_GRAPH_ROLL, gsm_graph_roll_status, gsm_graph_info)
+ * 7: gsm_get_state / gsm_set_state; rollout graphs emit every step's edges in
+ *    their one launch (no separate emit launch) */
+#define GSM_ABI_VERSION 7
 
 typedef enum gsm_status {
     GSM_OK = 0,
@@ -212,6 +214,31 @@ int gsm_step(gsm_handle *h, const void *actions, int action_fmt, void *stream);
  * state buffers, e.g. set_state). */
 int gsm_observe(gsm_handle *h, void *stream);
 
+/* The simulator state (SURVEY.md §8(b) gsm_get_state / gsm_set_state):
+ * device pointers of the caller; NULL members are skipped. Everything else
+ * the library keeps (the row / contact masks, node features, edges) is
+ * derived from it. */
+typedef struct gsm_state {
+    float *pos;               /* [B][E][2] */
+    float *vel;               /* [B][N][2] */
+    int32_t *step_count;      /* [B]       */
+    int32_t *episode;         /* [B]       */
+    float *ep_acc;            /* [B][2]    */
+    float *ep_last;           /* [B][2]    */
+    int32_t *env_shape;       /* [B]       ragged scenarios: N_env | scenario << 8 */
+} gsm_state;
+
+/* Checkpoint / injection of env state (what a reference caller does by
+ * reading or writing the world's entity states directly, core.py
+ * EntityState, SOURCES.txt:14). gsm_get_state copies the bound state into
+ * `out`. gsm_set_state copies `in` into the bound state and then runs
+ * gsm_observe, which re-derives every output and the derived per-position
+ * state (row masks, contact candidates) the next step relies on — the one
+ * call a non-Python caller needs after writing positions or velocities.
+ * Stream-ordered device-to-device copies; no synchronisation. */
+int gsm_get_state(gsm_handle *h, const gsm_state *out, void *stream);
+int gsm_set_state(gsm_handle *h, const gsm_state *in, void *stream);
+
 /* gsm_step / gsm_observe with their outputs redirected (gsm_outputs). */
 int gsm_step_into(gsm_handle *h, const void *actions, int action_fmt, const gsm_outputs *out, void *stream);
 int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream);
@@ -240,15 +267,19 @@ int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream);
 #define GSM_GRAPH_TIME_ENDS 8
 #define GSM_GRAPH_UNFUSED 16
 #define GSM_GRAPH_LAG_ONLY 32
-/* GSM_GRAPH_ROLL: all n_steps steps run in ONE launch, then the last step's
- * edge emission in a second (segmented configs with
- * one env per wave, e.g. 24 agents + 24 obstacles; the whole batch in one
- * residency round). Each wave keeps its env's state on chip across the steps;
- * workgroups hand the CSR edge-count prefix to each other through tagged
- * granules (bounded waits). Outputs after the graph are identical to the
- * lagged chain's (every step's edges are emitted). Combines with GSM_GRAPH_TIME_ENDS only (the events then bracket
- * the launch: gsm_graph_kernel_ms gives its time per step); GSM_EINVAL where
- * the config has no rollout kernel. */
+/* GSM_GRAPH_ROLL: all n_steps steps and their edges run in ONE launch
+ * (navigation configs with a compiled rollout shape — 3, 6, 12 or 24 agents
+ * with as many obstacles, one env per wave — or the tile path, one env per
+ * workgroup; the whole batch in one residency round). Each wave keeps its
+ * env's state on chip across the steps; workgroups hand the CSR edge-count
+ * prefix to each other through tagged granules (bounded waits), and a tail
+ * iteration emits the last step's edges. Outputs after the graph are
+ * identical to the lagged chain's (every step's edges are emitted; in the
+ * bound buffers the earlier steps' go to a library scratch of the bound edge
+ * capacity, allocated on first use, since a workgroup may trail its
+ * successors by steps). Combines with GSM_GRAPH_TIME_ENDS only (the events
+ * then bracket the launch: gsm_graph_kernel_ms gives its time per step);
+ * GSM_EINVAL where the config has no rollout kernel. */
 #define GSM_GRAPH_ROLL 64
 int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t action_stride_bytes,
                       int32_t n_actions, int32_t n_steps, int action_fmt, int flags);
@@ -264,9 +295,10 @@ int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream);
  * fused rollout launch (GSM_GRAPH_ROLL, or gsm_graph_capture_into on a
  * rollout buffer) rather than a per-step chain. */
 int gsm_graph_info(gsm_handle *h, int32_t slot, int32_t *steps, int32_t *fused);
-/* After GSM_GRAPH_ROLL launches have completed: *gave_up = 1 if any bounded
- * wait of a rollout launch timed out since the last call (its outputs are
- * then invalid), else 0. Clears the flag. */
+/* After graph launches have completed: *gave_up = 1 if any bounded in-launch
+ * wait (a rollout launch's CSR hand-off, or the ragged lagged chain's staging
+ * wait) timed out since the last call (that launch's edges are then invalid),
+ * else 0. Clears the flag. Synchronises (reads a device word). */
 int gsm_graph_roll_status(gsm_handle *h, int32_t *gave_up);
 /* After a timed launch of `slot` has completed: mean duration (ms) of the
  * step and emit kernels (TIME_EACH), and the whole graph (both flags). */

@@ -51,9 +51,10 @@ def test_struct_layouts_match_header(lib, tmp_path):
     fields_buf = [f for f, _ in _lib.GsmBuffers._fields_]
     fields_sz = [f for f, _ in _lib.GsmSizes._fields_]
     fields_out = [f for f, _ in _lib.GsmOutputs._fields_]
+    fields_st = [f for f, _ in _lib.GsmState._fields_]
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "gsm.h"', "int main(void){"]
     for s, fs in (("gsm_config", fields_cfg), ("gsm_buffers", fields_buf), ("gsm_sizes", fields_sz),
-                  ("gsm_outputs", fields_out)):
+                  ("gsm_outputs", fields_out), ("gsm_state", fields_st)):
         lines.append(f'printf("{s} %zu\\n", sizeof({s}));')
         for f in fs:
             lines.append(f'printf("{s}.{f} %zu\\n", offsetof({s}, {f}));')
@@ -64,7 +65,7 @@ def test_struct_layouts_match_header(lib, tmp_path):
     got = dict(l.rsplit(" ", 1) for l in subprocess.run([str(exe)], capture_output=True, text=True,
                                                          check=True).stdout.split("\n") if l)
     for s, cls in (("gsm_config", _lib.GsmConfig), ("gsm_buffers", _lib.GsmBuffers), ("gsm_sizes", _lib.GsmSizes),
-                   ("gsm_outputs", _lib.GsmOutputs)):
+                   ("gsm_outputs", _lib.GsmOutputs), ("gsm_state", _lib.GsmState)):
         assert int(got[s]) == C.sizeof(cls), s
         for f, _ in cls._fields_:
             assert int(got[f"{s}.{f}"]) == getattr(cls, f).offset, f"{s}.{f}"
@@ -102,6 +103,33 @@ def test_create_bind_destroy_host_only(lib):
     assert lib.gsm_bind(h, C.byref(bufs)) == _lib.GSM_EINVAL     # NULL pointers
     assert lib.gsm_destroy(h) == _lib.GSM_OK
     assert lib.gsm_destroy(None) == _lib.GSM_OK
+
+
+def test_capture_into_argument_checks_host_only(lib):
+    """gsm_graph_capture_into rejects a NULL handle, an unbound handle and a
+    bad slot before it touches a slot, a buffer or the GPU (a navigation bind
+    only records the pointers: fake non-NULL ones make no HIP call)."""
+    from gsmarl_amd import EnvConfig, _lib
+    outs = (_lib.GsmOutputs * 2)()
+    a = C.c_void_p(4096)
+    assert lib.gsm_graph_capture_into(None, 0, a, 16, 1, 2, 1, outs) == _lib.GSM_EINVAL
+    c = _lib.make_config(EnvConfig(n_agents=24, n_envs=4))
+    h = C.c_void_p()
+    assert lib.gsm_create(C.byref(c), C.byref(h)) == _lib.GSM_OK
+    assert lib.gsm_graph_capture_into(h, 0, a, 16, 1, 2, 1, outs) == _lib.GSM_ESTATE   # before bind
+    assert lib.gsm_graph_capture(h, 0, a, 16, 1, 2, 1, _lib.GRAPH_ROLL) == _lib.GSM_ESTATE
+    fake = {f: 4096 * (i + 1) for i, (f, _) in enumerate(_lib.GsmBuffers._fields_)}
+    fake["lsa_v"] = fake["lsa_col"] = fake["lsa_stats"] = fake["env_shape"] = fake["assign"] = None
+    bufs = _lib.GsmBuffers(**fake)
+    assert lib.gsm_bind(h, C.byref(bufs)) == _lib.GSM_OK
+    for bad in (-1, 4, 1 << 20):
+        assert lib.gsm_graph_capture_into(h, bad, a, 16, 1, 2, 1, outs) == _lib.GSM_EINVAL, bad
+        assert "slot" in _lib.last_error(lib, h)
+        assert lib.gsm_graph_capture(h, bad, a, 16, 1, 2, 1, _lib.GRAPH_ROLL) == _lib.GSM_EINVAL, bad
+    assert lib.gsm_graph_capture_into(h, 0, a, 16, 1, 2, 1, None) == _lib.GSM_EINVAL   # NULL per_step
+    assert lib.gsm_get_state(h, None, None) == _lib.GSM_EINVAL
+    assert lib.gsm_set_state(None, C.byref(_lib.GsmState()), None) == _lib.GSM_EINVAL
+    assert lib.gsm_destroy(h) == _lib.GSM_OK
 
 
 def test_product_path_fails_loudly_without_gpu():

@@ -3,9 +3,11 @@ a graph in one launch, workgroups handing the CSR edge-count prefix to each
 other through tagged granules. Every state and output buffer must equal the
 eager steps' (which test_gpu_parity checks against the oracle) bit for bit:
 partial workgroups, auto-resets (episode length 5 and 7), all three action
-formats, repeated replays (the granules are re-zeroed by the graph), and the
-headline batch (one residency round of 2048 workgroups), and the tile path's
-rollout (one 512-thread workgroup per env, C3's 96 agents). Also checked
+formats, repeated replays (granules tagged with a launch epoch), the headline
+batch (one residency round of 2048 workgroups), the reference's zero-shot
+sizes 6 and 12, and the tile path's rollout (one 512-thread workgroup per env,
+C3's 96 agents). The last step's edges are emitted by the rollout launch's
+tail iteration (no separate emit launch). Also checked
 against the CPU oracle directly at the end of a chain."""
 import numpy as np
 import pytest
@@ -57,6 +59,9 @@ def _same(ref, env, what):
                                           (24, 8192, 26, 25, "index"),
                                           # C2's shape (the step kernels pack 4 envs per wave, the rollout one)
                                           (3, 64, 12, 5, "index"), (3, 4096, 15, 6, "index"), (3, 4100, 7, 3, "onehot"),
+                                          # the reference's zero-shot navigation sizes (readme.md:75)
+                                          (6, 1024, 10, 4, "index"), (6, 37, 7, 3, "cont"), (12, 2048, 9, 5, "onehot"),
+                                          (12, 100, 6, 4, "index"),
                                           # tile path (one workgroup per env): C3's shape
                                           (96, 16, 9, 5, "index"), (96, 33, 6, 4, "onehot"), (96, 7, 5, 2, "cont"),
                                           (96, 1024, 12, 10, "index"), (70, 9, 3, 2, "index")])
@@ -109,7 +114,7 @@ def test_roll_emit_after_chain(N, B):
     env.close()
 
 
-@pytest.mark.parametrize("N,B", [(24, 48), (96, 12)])
+@pytest.mark.parametrize("N,B", [(24, 48), (96, 12), (6, 40), (12, 40)])
 def test_roll_oracle_direct(N, B):
     """The last step of a rollout graph vs the fp64 CPU oracle stepped from
     the identical fp32 pre-step state (eager steps reach it bit for bit):
@@ -208,3 +213,41 @@ def test_roll_episodes_match_chain(N, B):
     assert not env.roll_gave_up()
     _same(ref, env, "3 episodes")
     env.close()
+
+
+@pytest.mark.parametrize("N,B,T,mode", [(3, 100, 1, "slots"), (24, 100, 1, "bound"), (3, 100, 3, "slots"),
+                                        (24, 300, 2, "bound")])
+def test_roll_recycled_granules(N, B, T, mode):
+    """Back-to-back envs of one shape: each capture's granules are a fresh
+    allocation, usually at the address the previous env freed. Its granules
+    are initialised by agent-scope stores at a new epoch, so no granule of the
+    previous allocation is taken for this launch's (a hipMemset's zeros did
+    not hide them: the second env of a pair got the first's group sums)."""
+    from gsmarl_amd import GraphRolloutBuffer
+    for rep in range(3):
+        env, cfg = _env(n_agents=N, n_envs=B, seed=2, episode_length=6)
+        ref, _ = _env(n_agents=N, n_envs=B, seed=2, episode_length=6)
+        acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+        if mode == "slots":
+            gb, eb = GraphRolloutBuffer(env, episode_length=T), GraphRolloutBuffer(ref, episode_length=T)
+            gb.reset(seed=2)
+            gb.capture(acts)
+            gb.replay()
+            eb.reset(seed=2)
+            for t in range(T):
+                eb.insert(acts[t])
+            torch.cuda.synchronize()
+            got, want = gb.edge_ptr, eb.edge_ptr
+        else:
+            env.reset(seed=2)
+            env.capture(acts, T, slot=0, kernels="roll")
+            env.replay(0)
+            ref.reset(seed=2)
+            for t in range(T):
+                ref.step(acts[t], sync_edges=False)
+            torch.cuda.synchronize()
+            got, want = env.t["edge_ptr"], ref.t["edge_ptr"]
+        assert not env.roll_gave_up()
+        assert torch.equal(got, want), (rep, (got != want).nonzero().flatten()[:8].tolist())
+        env.close()
+        ref.close()

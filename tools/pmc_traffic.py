@@ -4,9 +4,9 @@ bench.py reads for roofline.traffic and roofline.valu_frac.
 Per kernel: HBM bytes per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes;
 the x2 is the gfx950 FETCH_SIZE correction of MI355X_MICROARCH.md section
 HBM/rocprofv3), VALU / SALU / LDS instructions per launch and waves. The file
-records the hash of the kernel sources it was collected on (bench.kernel_src_hash);
-bench.py ignores it once the sources change, so stale counters never reach a
-bench line.
+records the hash of the device code it was collected on (bench.code_object_hash:
+the .hip_fatbin of the built libgsm.so); bench.py ignores it once the device
+code changes, so stale counters never reach a bench line.
 
 The fused rollout kernel ("roll") runs ROLL_STEPS steps per launch (env,
 default 100: a 100-step graph); its entry is normalised to one step, so that
@@ -23,14 +23,15 @@ import time
 from pathlib import Path
 
 sys.path.insert(0, str(Path(__file__).resolve().parents[1]))
-from bench import kernel_src_hash  # noqa: E402
+sys.path.insert(0, str(Path(__file__).resolve().parents[1] / "gs-marl_amd"))
+from bench import code_object_hash  # noqa: E402
 
 out_path = sys.argv[1]
-h = kernel_src_hash()
+h = code_object_hash()
 res = json.load(open(out_path)) if os.path.exists(out_path) else {}
-if res.get("src_hash") != h:   # entries from other sources are dropped, not mixed
+if res.get("code_object_hash") != h:   # entries from other builds are dropped, not mixed
     res = {}
-res.update(src_hash=h, collected=time.strftime("%Y-%m-%d %H:%M:%S"))
+res.update(code_object_hash=h, collected=time.strftime("%Y-%m-%d %H:%M:%S"))
 ent = res.setdefault("entries", {})
 for spec in sys.argv[2:]:
     key, d = spec.split("=", 1)

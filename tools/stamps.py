@@ -1,4 +1,4 @@
-"""Per-phase wave timelines from a -DGSM_STAMPS build (tools/ablate.sh build
+"""Per-phase wave timelines from a -DGSM_STAMPS build (tools/build_variant.sh
 "stamps:-DGSM_STAMPS"). Runs one timed 100-step graph on the headline config
 and summarises the last step's stamps (diagnostic only; stamps perturb timing).
 Step-kernel phases (gsm_seg_kernels.hip): 0 entry, 1 inputs staged, 2 lagged

@@ -1,5 +1,5 @@
 """Per-wave cycles and path iterations of the ragged kernel's assignment
-(diagnostic -DGSM_STAMPS build: tools/ablate.sh build "stamps:-DGSM_STAMPS",
+(diagnostic -DGSM_STAMPS build: tools/build_variant.sh "stamps:-DGSM_STAMPS",
 run with GSM_LIB_PATH pointing at it): one step of a polygon batch (ABL_N
 agents, ABL_B envs), then the median s_memtime cycles spent in wave_lsa, the
 median / max path iterations and the cycles per iteration."""
