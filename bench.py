@@ -154,6 +154,25 @@ def ragged_kernel_bytes(env, EL, action_bytes, total_edges):
     return step, emit, lag
 
 
+def ragged_roll_step_bytes(env, EL, action_bytes, total_edges):
+    """Algorithmic HBM bytes per step of the ragged fused rollout launch,
+    summed over the batch's env shapes: the step's actions and observation
+    outputs (6 node-feature floats per agent, reward / cost / assign over
+    N_max, done, the edge_ptr entry, 12 B per edge), the assignment's
+    warm-start state of polygon/line envs (f64 column dual + int32 matching
+    per agent, read and written), the static node rows of a reset amortised
+    over the episode. The simulator state stays on chip (loaded / stored once
+    per launch, left out); the per-env edge slabs the launch packs from are
+    its own staging, not algorithmic traffic."""
+    import numpy as np
+    sh = env.t["env_shape"].cpu().numpy()
+    n, scn = (sh & 0xFF).astype(np.int64), sh >> 8
+    Nmax, Emax = env.N, env.E
+    per = action_bytes * n + 24 * n + 12 * Nmax + 1 + 8 + (28 * Emax + 4) / EL
+    warm = np.where(scn != 0, 2 * 12 * n, 0) if env.cfg.lsa_warm_start else 0
+    return float((per + warm).sum()) + 12 * total_edges
+
+
 CONFIGS = {   # BASELINE.json configs runnable as a one-GPU bench line
     "h": dict(scenario="navigation", n_agents=24, n_envs=8192, desc="BASELINE headline / configs[4] shard"),
     "c2": dict(scenario="navigation", n_agents=3, n_envs=4096, desc="BASELINE configs[1]"),
@@ -600,8 +619,9 @@ def run_rank(args):
                        "episode_length": EL, "mean_edges_per_env": round(total_edges / B, 2),
                        "parallelism": f"env-sharded x{world} (no data-path collective)",
                        "launch": "eager" if args.eager else (f"hip-graphs of {chunk} steps" + (
-                           ": all steps of a graph in one fused rollout launch (state on chip, in-launch CSR "
-                           "prefix) + the last step's emit launch"
+                           (": all steps of a graph and their edges in one fused rollout launch (state on chip; "
+                            + ("each env packs its edges a few steps behind its own step through a slab, "
+                               "per-wave CSR prefix granules)" if cfg.ragged else "in-launch CSR look-back)"))
                            if roll else ", lagged emission (one launch per step)" if ((seg_cfg or cfg.ragged)
                                                                                      and not args.unfused)
                            else ", step + emit launch per step"))},
@@ -648,6 +668,9 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False):
         if lag:
             sb += lb
         names = ("gsm_step_ragged_kernel" + ("<lagged emission>" if lag else ""), "gsm_emit_ragged_kernel")
+        if roll:
+            sb = ragged_roll_step_bytes(env, EL, 4, edges_now)
+            names = (f"gsm_roll_ragged_kernel (per step of a {L}-step launch)", names[1])
     elif roll:
         sb = roll_step_bytes(B, N, cfg.n_obstacles, EL, 4, edges_now, seg)
         eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)

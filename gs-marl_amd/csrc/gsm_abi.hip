@@ -7,6 +7,7 @@
 // gsm_step / gsm_reset / gsm_observe.
 #include <math.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -51,6 +52,8 @@ struct gsm_handle {
     } slots[GSM_GRAPH_SLOTS];
     uint32_t *roll_status = nullptr;  // fused rollout: a bounded wait gave up (sticky until read)
     void *edge_scratch = nullptr;     // fused rollout in the bound buffers: edges of all but the last step
+    void *slab = nullptr;             // ragged rollout: per-env edge slabs (depth + 1 steps)
+    size_t slab_bytes = 0;
 };
 
 namespace {
@@ -581,9 +584,11 @@ int gsm_graph_capture_into(gsm_handle *h, int32_t slot, const void *actions, int
 
 
 // Fused rollout graph (GSM_GRAPH_ROLL): ONE gsm_roll_seg_kernel /
-// gsm_roll_tile_kernel launch for all n_steps steps and all their edges (the
-// last step's emitted by a tail iteration; that launch also advances the
-// granule epoch). Every output equals the lagged chain's.
+// gsm_roll_tile_kernel / gsm_roll_ragged_kernel launch for all n_steps steps
+// and all their edges (a tail after the loop emits the last ones; that launch
+// also advances the granule epoch). Every output equals the per-step chain's.
+// The ragged rollout packs each step's edges `depth` steps late
+// (GSM_ROLL_DEPTH, default 4, 2..kRaggedRollMaxDepth).
 static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_t stride, int32_t n_actions,
                         int32_t n_steps, int action_fmt, int flags, const gsm_outputs *per_step, bool fallback) {
     // every caller checks these first; repeated so that no path reaches the
@@ -601,17 +606,18 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     p.action_fmt = action_fmt;
     p.env_mask = nullptr;
     p.reseed = 0;
-    const bool tile = p.path == gsm::kPathTile;
+    const bool tile = p.path == gsm::kPathTile, ragged = p.path == gsm::kPathRagged;
     const bool slots = per_step != nullptr;
-    const void *roll_fn = tile ? gsm::roll_tile_kernel_fn(p, slots) : gsm::roll_seg_kernel_fn(p, slots);
+    const void *roll_fn = tile ? gsm::roll_tile_kernel_fn(p, slots)
+                               : ragged ? gsm::roll_ragged_kernel_fn(p, slots) : gsm::roll_seg_kernel_fn(p, slots);
     if (!roll_fn && fallback) return kRollIneligible;
     if (!roll_fn) return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: no fused rollout kernel for this config "
-                                             "(segmented path with a compiled shape, or tile path with the "
-                                             "symmetric sweep)");
+                                             "(segmented path with a compiled shape, tile path with the "
+                                             "symmetric sweep, or a ragged batch)");
     // step k's outputs at base + k * stride (a rollout buffer's slots) or all
     // in the bound buffers
     gsm::DevParams::RollOut ro{p.node_feat, p.reward, p.cost, p.done, p.edge_count, p.edge_ptr, p.edge_index,
-                               p.edge_attr, 0, 0, 0, 0, 0, 0, 0, p.edge_capacity, nullptr, nullptr};
+                               p.edge_attr, 0, 0, 0, 0, 0, 0, 0, p.edge_capacity, nullptr, nullptr, p.assign, 0};
     if (per_step) {
         int64_t cost_s = 0;
         bool ok = slot_field(per_step, n_steps, &gsm_outputs::node_feat, &ro.nf, &ro.nf_s) &&
@@ -622,7 +628,8 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
                   slot_field(per_step, n_steps, &gsm_outputs::edge_ptr, &ro.eptr, &ro.ep_s) &&
                   slot_field(per_step, n_steps, &gsm_outputs::edge_index, &ro.eidx, &ro.ei_s) &&
                   slot_field(per_step, n_steps, &gsm_outputs::edge_attr, &ro.eattr, &ro.ea_s) &&
-                  cost_s == ro.rc_s && !per_step[0].assign;
+                  cost_s == ro.rc_s && (ragged ? slot_field(per_step, n_steps, &gsm_outputs::assign, &ro.asg, &ro.as_s)
+                                               : !per_step[0].assign);
         for (int j = 0; ok && j < n_steps; ++j) {
             const int rc = redirect(h, &p, &per_step[j]);   // validates the slot
             if (rc) return rc;
@@ -635,9 +642,10 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         if (per_step[0].edge_index) ro.cap = per_step[0].edge_capacity;
         // p now describes the last slot: the final emit launch writes it
     }
-    // segmented rollout: one env per wave whatever the config's G (4 per workgroup)
+    // segmented / ragged rollout: one env per wave whatever the config's G (4 per workgroup)
     const int nb = tile ? gsm::step_grid_blocks(p) : (p.B + gsm::kWavesPerBlock - 1) / gsm::kWavesPerBlock;
-    const size_t roll_lds = tile ? gsm::roll_tile_kernel_lds(p) : gsm::roll_kernel_lds(p);
+    const size_t roll_lds = tile ? gsm::roll_tile_kernel_lds(p)
+                                 : ragged ? gsm::roll_ragged_kernel_lds(p) : gsm::roll_kernel_lds(p);
     // every workgroup resident at once (one residency round; a workgroup only
     // waits on lower-numbered ones, so this is for speed, not for progress)
     int dev = 0, per_cu = 0, n_cu = 0;
@@ -651,20 +659,40 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: the batch exceeds one residency round of the rollout kernel");
     }
     const int K = n_steps;
-    // tags carry the step in 12 bits (one env per wave) or 16 (tile); checked
-    // before the slot's graph is dropped
-    const int max_k = tile ? 65535 : gsm::kXferMaxSteps;
+    // tags carry the step in 12 bits (ragged: per-wave granules) or 16
+    // (look-back granules); checked before the slot's graph is dropped
+    const int max_k = ragged ? gsm::kXferMaxSteps : 65535;
     if (K > max_k) {
         if (fallback) return kRollIneligible;
-        return fail(h, GSM_EINVAL, tile ? "GSM_GRAPH_ROLL: n_steps must be <= 65535"
-                                        : "GSM_GRAPH_ROLL: n_steps must be <= 4095");
+        return fail(h, GSM_EINVAL, ragged ? "GSM_GRAPH_ROLL: n_steps must be <= 4095"
+                                          : "GSM_GRAPH_ROLL: n_steps must be <= 65535");
     }
-    // one env per wave: per-wave granules, groups of 64 waves (at most 128
-    // groups: one residency round holds <= 8192 waves)
+    // ragged: per-wave granules, groups of 64 waves (at most 128 groups: one
+    // residency round holds <= 8192 waves), edges packed `depth` steps late
     const int xW = nb * gsm::kWavesPerBlock, xNG = (xW + gsm::kWave - 1) / gsm::kWave;
-    if (!tile && xNG > 2 * gsm::kWave) {
+    if (ragged && xNG > 2 * gsm::kWave) {
         if (fallback) return kRollIneligible;
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: more than 8192 envs in one rollout launch");
+    }
+    int depth = 0;
+    if (ragged) {
+        depth = 4;
+        if (const char *ev = getenv("GSM_ROLL_DEPTH")) depth = atoi(ev);
+        depth = std::min(std::max(depth, 2), gsm::kRaggedRollMaxDepth);
+        // the env slabs of depth + 1 steps (each env's edges at a fixed stride)
+        const size_t need = (size_t)(depth + 1) * p.B * 12 * (size_t)h->sz.max_edges_per_env;
+        if (h->slab_bytes < need) {
+            if (h->slab) (void)hipFree(h->slab);
+            h->slab = nullptr;
+            h->slab_bytes = 0;
+            e = hipMalloc(&h->slab, need);
+            if (e != hipSuccess) {
+                h->slab = nullptr;
+                if (fallback) return kRollIneligible;
+                return hip_fail(h, e, "hipMalloc (rollout edge slabs)");
+            }
+            h->slab_bytes = need;
+        }
     }
     if (!h->roll_status) {
         e = hipMalloc(&h->roll_status, 16);
@@ -687,12 +715,13 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     }
     gsm_handle::Slot &sl = h->slots[slot];
     drop_slot(sl);
-    // a 16-byte header (the launch epoch), then one env per wave: per-wave
-    // counts [K][xW] and group sums [K][xNG] (32-bit granules); tile: aggregates
-    // [K][nb] and inclusive prefixes [K][nb] (look-back). Zeroed once here —
-    // granules are tagged with the launch epoch, so replays never clear them
-    const size_t gran_alloc = tile ? 16 + 2 * (size_t)K * nb * sizeof(uint64_t)
-                                   : 16 + (size_t)K * (xW + xNG) * sizeof(uint32_t);
+    // a 16-byte header (the launch epoch), then ragged: per-wave counts
+    // [K][xW] and group sums [K][xNG] (32-bit granules); segmented / tile:
+    // aggregates [K][nb] and inclusive prefixes [K][nb] (look-back). Zeroed
+    // once here — granules are tagged with the launch epoch, so replays never
+    // clear them
+    const size_t gran_alloc = ragged ? 16 + (size_t)K * (xW + xNG) * sizeof(uint32_t)
+                                     : 16 + 2 * (size_t)K * nb * sizeof(uint64_t);
     e = hipMalloc(&sl.gran, gran_alloc);
     if (e != hipSuccess) {
         sl.gran = nullptr;
@@ -730,8 +759,9 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     }
     p.actions = actions;
     p.ro = ro;
-    p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, xW, xNG, 0, sl.gran + 2,
-                                  h->roll_status, (uint32_t *)sl.gran};
+    p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, xW, xNG, depth,
+                                  h->sz.max_edges_per_env, 0, sl.gran + 2, h->roll_status, (uint32_t *)sl.gran,
+                                  (int32_t *)h->slab};
     if (e == hipSuccess) {
         what = "rollout kernel node";
         hipKernelNodeParams kp = {};
@@ -1034,6 +1064,7 @@ int gsm_destroy(gsm_handle *h) {
     if (h->bsum_alt) (void)hipFree(h->bsum_alt);
     if (h->roll_status) (void)hipFree(h->roll_status);
     if (h->edge_scratch) (void)hipFree(h->edge_scratch);
+    if (h->slab) (void)hipFree(h->slab);
     if (h->order_copied) (void)hipEventSynchronize(h->order_copied);
     if (h->block_order) (void)hipFree(h->block_order);
     if (h->order_host) (void)hipHostFree(h->order_host);

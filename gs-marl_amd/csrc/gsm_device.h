@@ -235,18 +235,42 @@ __device__ __forceinline__ uint64_t roll_wait(const uint64_t *g, uint32_t tag, u
     }
 }
 
-// ---- per-wave CSR hand-off of the one-env-per-wave rollouts (lag-2 emission)
+// Environment._set_action + apply_action_force of a rollout step: agent index
+// `a` of action row `row` (roll.actions + row * stride), runtime format.
+template <typename Params>   // DevParams or its kernarg view (late_params)
+__device__ __forceinline__ float2 roll_action_force(const Params &p, int row, int64_t a) {
+    const char *base = p.roll.actions + (int64_t)row * p.roll.stride;
+    float ux, uy;
+    if (p.action_fmt == 0) {
+        const float *q = (const float *)base + a * 5;
+        ux = q[1] - q[2];
+        uy = q[3] - q[4];
+    } else if (p.action_fmt == 1) {
+        const int k = ((const int32_t *)base)[a];
+        ux = (float)(k == 1) - (float)(k == 2);
+        uy = (float)(k == 3) - (float)(k == 4);
+    } else {
+        const float2 q = ((const float2 *)base)[a];
+        ux = q.x;
+        uy = q.y;
+    }
+    return make_float2(ux * p.sens, uy * p.sens);
+}
+
+// ---- per-wave CSR hand-off of the one-env-per-wave rollouts
 //
-// The packed CSR offset of env (= wave) w at step s is the sum of the edge
-// counts of every wave before it. Three levels, all 32-bit granules
+// (the ragged rollout, gsm_ragged_kernels.hip; `depth` = the lag between a
+// step and the packing of its edges, >= 2). The packed CSR offset of env (=
+// wave) w at step s is the sum of the edge counts of every wave before it.
+// Three levels, all 32-bit granules
 // {tag12 << 20 | value20} stored and loaded with relaxed agent-scope atomics
 // (write-through, no fence):
 //   agg[s][w]  wave w's edge count at step s, published right after its sweep;
 //   grp[s][g]  the sum of agg[s][64g .. 64g+63], published by wave 64g+63 in
 //              iteration s + 1 (its loads issued at the top of that iteration);
 //   offset     sum of grp[s][g' < w/64] + sum of agg[s][64(w/64) .. w-1],
-//              loaded at the top of iteration s + 2 and summed at its end,
-//              when step s's edges are emitted.
+//              loaded at the top of iteration s + depth and summed at its
+//              end, when step s's edges are packed.
 // Every granule a wave reads was published at least one iteration before it
 // is needed, so the loads' latency hides behind a whole step and no wave waits
 // in the normal case; there are no barriers. A wave waits only on waves of

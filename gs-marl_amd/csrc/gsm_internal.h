@@ -102,11 +102,13 @@ struct DevParams {
         const char *actions;
         int64_t stride;
         int32_t n_actions, t_first, K;
-        int32_t xW, xNG;      // one-env-per-wave rollouts: waves of the grid, groups of 64 (gsm_device.h Xfer)
-        int32_t pad;
+        int32_t xW, xNG;      // per-wave hand-off (ragged rollout): waves of the grid, groups of 64 (gsm_device.h Xfer)
+        int32_t depth;        // ragged rollout: steps between an env's step and the packing of its edges
+        int32_t slab_e, pad;  // ragged rollout: edges per env slab (the config's max_edges_per_env)
         uint64_t *gran;
         uint32_t *status;
         uint32_t *epoch;
+        int32_t *slab;        // ragged rollout: [depth + 1][B] slabs of [2][slab_e] int32 + [slab_e] f32
     } roll;
     // A rollout's per-step outputs: step k's at base + k * stride (elements;
     // stride 0 = every step into the bound buffers, > 0 = a rollout buffer's
@@ -126,6 +128,8 @@ struct DevParams {
         int64_t nf_s, rc_s, done_s, ec_s, ep_s, ei_s, ea_s, cap;
         int32_t *eidx_mid;
         float *eattr_mid;
+        int32_t *asg;         // ragged: assignment [B][N] of step k at asg + k * as_s
+        int64_t as_s;
     } ro;
 };
 
@@ -168,6 +172,11 @@ size_t roll_kernel_lds(const DevParams &p);
 const void *roll_tile_kernel_fn(const DevParams &p, bool slots);   // nullptr unless p.tile_sym
 size_t roll_tile_kernel_lds(const DevParams &p);
 const void *step_ragged_kernel_fn();
+// fused K-step rollout of a ragged batch (one env per wave, edges packed
+// `depth` steps behind through per-env slabs) and its LDS bytes
+const void *roll_ragged_kernel_fn(const DevParams &p, bool slots);
+size_t roll_ragged_kernel_lds(const DevParams &p);
+constexpr int kRaggedRollMaxDepth = 8;
 const void *lag_step_ragged_kernel_fn();   // kLag: the previous step's emission first
 const void *step_tile_kernel_fn();
 const void *emit_tile_kernel_fn();

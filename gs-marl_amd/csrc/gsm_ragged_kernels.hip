@@ -105,7 +105,8 @@ struct RShape {
     float L, twoL;               // layout half-width
 };
 
-__device__ __forceinline__ RShape make_shape(const DevParams &p, int N, int scn) {
+template <typename Params>
+__device__ __forceinline__ RShape make_shape(const Params &p, int N, int scn) {
     RShape s;
     s.N = N;
     s.scn = scn;
@@ -119,7 +120,8 @@ __device__ __forceinline__ RShape make_shape(const DevParams &p, int N, int scn)
 }
 
 // N_env and scenario of global env id gid (oracle/ragged_ref.py: env_shapes)
-__device__ __forceinline__ RShape draw_shape(const DevParams &p, int b) {
+template <typename Params>
+__device__ __forceinline__ RShape draw_shape(const Params &p, int b) {
     const int64_t gid = p.env_base + b;
     int N = p.N, scn = p.scenario;
     if (p.scenario == kScnMixed) {
@@ -130,19 +132,22 @@ __device__ __forceinline__ RShape draw_shape(const DevParams &p, int b) {
     return make_shape(p, N, scn);
 }
 
-__device__ __forceinline__ float2 layout_at(const DevParams &p, const RShape &s, uint32_t gid, uint32_t ep,
+template <typename Params>
+__device__ __forceinline__ float2 layout_at(const Params &p, const RShape &s, uint32_t gid, uint32_t ep,
                                             uint32_t e) {
     const Philox4 x = philox4x32_10(e, ep, gid, kTagLayout, p.seed_lo, p.seed_hi);
     return make_float2(u01(x.x0) * s.twoL - s.L, u01(x.x1) * s.twoL - s.L);
 }
 
 // storage row of collider l (agents, then obstacles)
-__device__ __forceinline__ int collider_row(const DevParams &p, const RShape &s, int l) {
+template <typename Params>
+__device__ __forceinline__ int collider_row(const Params &p, const RShape &s, int l) {
     return l < s.N ? l : p.N + p.T + (l - s.N);
 }
 
 // slot j (< N) of a polygon/line env from its target positions (lanes 0/1)
-__device__ __forceinline__ float2 slot_of(const DevParams &p, const RShape &s, int lane, float2 tp) {
+template <typename Params>
+__device__ __forceinline__ float2 slot_of(const Params &p, const RShape &s, int lane, float2 tp) {
     const int j = lane < s.N ? lane : 0;
     if (s.scn == kScnPolygon) {
         const float2 c = rl_f2(tp, 0);
@@ -213,6 +218,10 @@ __device__ __forceinline__ LsaLds lsa_lds(unsigned char *lds, int nmax) {
                   (int *)(lds + cb + 16 * kRaggedMaxAgents), S};
 }
 
+// kColLds: the path loop reads C[i][lane] from the LDS copy instead of a
+// 32-register column (the rollout kernel's 64-VGPR budget; one LDS read on the
+// loop's chain, same values: identical results).
+template <bool kColLds = false>
 __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &sl, float *own, LsaWarm w,
                         int *iters = nullptr, uint64_t *tm = nullptr) {
     const bool col = lane < N;
@@ -231,24 +240,28 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
     // Rows in groups of 8 with no per-row branch, so the (correctly rounded)
     // square roots of a group are independent instructions; rows >= N of the
     // last group are computed and never read.
-    float ccol[kRaggedMaxAgents];
+    float ccol[kColLds ? 1 : kRaggedMaxAgents];
 #pragma unroll
     for (int i0 = 0; i0 < kRaggedMaxAgents; i0 += 8) {
         if (i0 < N) {
+            float c8[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
                 const float2 pi = rl_f2(pa, i0 + k);
                 const float dx = pi.x - slot.x, dy = pi.y - slot.y;
-                ccol[i0 + k] = sqrtf(dx * dx + dy * dy);
+                c8[k] = sqrtf(dx * dx + dy * dy);
             }
 #pragma unroll
-            for (int k = 0; k < 8; ++k)
-                if (col) s_cost[(i0 + k) * S + lane] = ccol[i0 + k];
-        } else {
+            for (int k = 0; k < 8; ++k) {
+                if (col) s_cost[(i0 + k) * S + lane] = c8[k];
+                if constexpr (!kColLds) ccol[i0 + k] = c8[k];
+            }
+        } else if constexpr (!kColLds) {
 #pragma unroll
             for (int k = 0; k < 8; ++k) ccol[i0 + k] = 0.0f;
         }
     }
+    const int ccl = col ? lane : 0;   // kColLds: this lane's column (lanes past N read column 0, never used)
     wave_sync();
     LSA_T(0);
     const double kInf = __builtin_inf();
@@ -291,7 +304,8 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
 #endif
             srm |= 1ull << i;
             const double ui = rl_d(u, i);
-            const double r = minVal + (double)ccol[i] - ui - v;
+            const float cij = kColLds ? s_cost[i * S + ccl] : ccol[i];
+            const double r = minVal + (double)cij - ui - v;
             // selects on SGPR lane masks (remm, the update ballot), no per-lane
             // bit extraction on the chain
             const int rkey = f32_order_key((float)r + 0.0f);
@@ -788,7 +802,8 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
     return edges;
 }
 
-__device__ void ragged_env_emit_rows(const DevParams &p, const int b, const int lane, const int64_t off,
+template <typename Params>
+__device__ void ragged_env_emit_rows(const Params &p, const int b, const int lane, const int64_t off,
                                      const float2 *s_pos, const RShape &s, uint64_t mask, const EdgeSink &out);
 
 // kLag (graph chains, gsm_abi.hip capture_impl): the kernel also emits the
@@ -925,7 +940,8 @@ __global__ __launch_bounds__(kBlock) void gsm_step_ragged_kernel(DevParams p) {
 // ---------------------------------------------------------------------------
 // env b's edges at global offset `off` from its positions staged in LDS
 // (s_pos, all E_max rows) and its collider lanes' row masks
-__device__ void ragged_env_emit_rows(const DevParams &p, const int b, const int lane, const int64_t off,
+template <typename Params>
+__device__ void ragged_env_emit_rows(const Params &p, const int b, const int lane, const int64_t off,
                                      const float2 *s_pos, const RShape &s, const uint64_t mask,
                                      const EdgeSink &out) {
     const int Nmax = p.N, Tmax = p.T, Emax = p.E;
@@ -1022,6 +1038,403 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_ragged_kernel(DevParams p) {
         if (b == p.B - 1) p.edge_ptr[p.B] = off + p.edge_count[b];
     }
     ragged_env_emit(p, b, lane, off, smem + wave * p.wave_lds_emit, EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity});
+}
+
+// ---------------------------------------------------------------------------
+// Fused rollout of a ragged batch (GSM_GRAPH_ROLL; config C4)
+// ---------------------------------------------------------------------------
+// K steps of a graph chain in ONE launch, one env per wave (the wave's index
+// in the grid IS its env: identity order), every env's state on chip across
+// the steps: collider / target positions and velocities in registers, shape
+// and counters in SGPRs; the assignment's warm-start state stays in its
+// global buffers. Each step runs exactly the operations of
+// ragged_env_step (physics, radius sweep, per-step assignment, reward, cost,
+// auto-reset, node features): bit-identical outputs.
+//
+// What a per-step launch cannot do: let an env run ahead of the others. The
+// only thing envs share is the packed CSR offset of their edges, which needs
+// the edge counts of every earlier env. So a wave writes its env's edges of
+// step t into a slab of its own (fixed stride, in HBM) right after its sweep,
+// publishes its count (gsm_device.h Xfer, per-wave granules, group sums), and
+// packs the slab into the CSR outputs `depth` steps later, from granules
+// loaded at the top of that iteration. A wave whose assignment falls back to
+// the cold recurrence (an exact float32 tie) falls behind by a
+// few steps without holding anyone: its successors wait only if it is more
+// than `depth` steps behind. No barriers. A tail packs the last `depth`
+// steps. In the bound buffers the earlier steps' edges go to the library
+// scratch (roll_edge_sink): only the last step's may land in the shared
+// outputs.
+// per wave after the step kernel's LDS: the stashed lane state, the counts
+// (N_max = 24 mixed: 3616 + 1072 B per wave, 18.8 KB per workgroup: eight
+// workgroups per CU, so 8192 envs take one residency round)
+constexpr int kRaggedRollWaveLds = 16 * kRaggedMaxAgents + 8 * kWave + ((4 * (kRaggedRollMaxDepth + 1) + 15) & ~15);
+template <bool kSlots>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void gsm_roll_ragged_kernel(
+    DevParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int w = (int)blockIdx.x * kWavesPerBlock + wave;   // the env
+    const int Nmax = p.N, Tmax = p.T, Emax = p.E;
+    const bool live = w < p.B;
+    const int64_t eb = live ? w : 0;
+    unsigned char *lds = smem + wave * (p.wave_lds_step + kRaggedRollWaveLds);
+    const LsaLds s_lsa = lsa_lds(lds, Nmax);                    // assignment scratch
+    float2 *s_pos = (float2 *)(lds + lsa_lds_bytes(Nmax));      // [E] staged rows
+    float4 *s_stash = (float4 *)(lds + p.wave_lds_step);        // [32] lane state across the assignment
+    uint64_t *s_rm = (uint64_t *)(s_stash + kRaggedMaxAgents);   // [64]
+    int *s_cnt = (int *)(s_rm + kWave);                          // [depth + 1] the env's edge counts by step
+    const int D = p.roll.depth, K = p.roll.K, n_act = p.roll.n_actions;
+    int lane = threadIdx.x & 63;
+
+    // ---- the state before step t_first
+    int t = 0, ep = 0;
+    float2 acc = make_float2(0.0f, 0.0f), cp = acc, tp = acc, v = acc;
+    RShape s = make_shape(p, 0, kScnNav);                       // an idle wave: no agents, no edges
+    if (live) {
+        t = p.step_count[eb];
+        ep = p.episode[eb];
+        acc = p.ep_acc[eb];
+        const int32_t sh = p.env_shape[eb];
+        s = make_shape(p, sh & 0xFF, sh >> 8);
+        const float2 *pos_b = p.pos + eb * Emax;
+        if (lane < s.M) cp = pos_b[collider_row(p, s, lane)];
+        if (lane < s.T) tp = pos_b[Nmax + lane];
+        if (lane < s.N) v = p.vel[eb * Nmax + lane];
+    }
+    const uint32_t xbase = *p.roll.epoch * (uint32_t)K;
+    auto xf = [&]() -> Xfer {
+        KernargParams &q = late_params();
+        Xfer x;
+        x.W = q.roll.xW;
+        x.NG = q.roll.xNG;
+        x.agg = (uint32_t *)(q.roll.gran + 2);
+        x.grp = x.agg + (int64_t)q.roll.K * x.W;
+        x.status = q.roll.status;
+        x.base = xbase;
+        return x;
+    };
+    // launch parameters read at the point of use (late_params): held across
+    // the loop they would not fit the 78-SGPR / 64-VGPR budget
+    auto P = [&]() -> KernargParams & { return late_params(); };
+    // the env's edge slab at ring position j (step mod depth + 1): [2][slab_e]
+    // int32 node ids, [slab_e] f32
+    auto slab_of = [&](const int j) -> EdgeSink {
+        KernargParams &q = late_params();
+        const int64_t per = 3 * (int64_t)q.roll.slab_e;
+        int32_t *base = q.roll.slab + ((int64_t)j * q.B + eb) * per;
+        return EdgeSink{base, (float *)(base + 2 * q.roll.slab_e), q.roll.slab_e};
+    };
+    int ring = 0;                    // k mod (depth + 1): the slab / count of the current step
+    const bool glast = (w & 63) == 63;
+    int arow = p.roll.t_first % n_act;
+    int cur_edges = 0;              // the env's edge count of the current step
+    uint64_t rmask = 0;             // row masks of the current step (collider lanes)
+    bool coinc = false, relaid_any = false;
+
+    // radius row masks and collision counts (as ragged_env_step)
+    auto pair_sweep = [&](int *cnt) {
+        uint64_t rm = 0;
+        int n = 0;
+        bool z = false;
+        for (int c = 0; c < s.M; ++c) {
+            const float2 q = rl_f2(cp, c);
+            const float dx = cp.x - q.x, dy = cp.y - q.y;
+            const float d2 = dx * dx + dy * dy;
+            const bool other = c != lane;
+            n += (other && d2 < (c < s.N ? P().dmin2_aa : P().dmin2_ao)) ? 1 : 0;
+            rm |= (other && d2 > 0.0f && d2 <= P().R2) ? (1ull << c) : 0ull;
+            z |= other && d2 == 0.0f && c < s.N;
+        }
+        *cnt = n;
+        coinc = __any(lane < s.M && z);
+        return lane < s.M ? rm : 0ull;
+    };
+    // step k's edge count published, its edges written to the env's slab
+    auto publish = [&](const int k) {   // at ring position `ring`
+        const int edges = wave_sum((int)__popcll(rmask)) + 2 * s.N * s.Tper;
+        if (lane == 0) {
+            const Xfer x = xf();
+            xfer_st(x.agg + (int64_t)k * x.W + w, x.tag(k), (uint32_t)edges);
+            s_cnt[ring] = edges;
+        }
+        if (lane < s.M) s_pos[collider_row(P(), s, lane)] = cp;
+        if (lane < s.T) s_pos[Nmax + lane] = tp;
+        wave_sync();
+        if (live) ragged_env_emit_rows(P(), w, lane, 0, s_pos, s, rmask, slab_of(ring));
+        wave_sync();
+        cur_edges = edges;
+    };
+    // step j's edges packed into the CSR outputs at offset `off`
+    auto pack = [&](const int j, const int off_in) {   // step j = k - depth: ring position ring + 1
+        const int jr = ring == D ? 0 : ring + 1;
+        const int cnt = s_cnt[jr];
+        int64_t off = off_in;
+        if (off < 0) {   // a broken hand-off: never write out of bounds
+            if (lane == 0) __hip_atomic_store((gu32 *)P().roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            off = P().ro.cap;
+        }
+        if (!live) return;
+        KernargParams &q = late_params();
+        if (lane == 0) {
+            int64_t *const eptr = q.ro.eptr + (kSlots ? j * q.ro.ep_s : 0);
+            eptr[w] = off;
+            if (w == q.B - 1) eptr[q.B] = off + cnt;
+        }
+        const EdgeSink src = slab_of(jr), dst = roll_edge_sink<kSlots>(q, j, K);
+        for (int e = lane; e < cnt; e += kWave) {
+            if (off + e < dst.cap) {   // a redirected slot may be smaller than the worst case
+                dst.index[off + e] = src.index[e];
+                dst.index[dst.cap + off + e] = src.index[src.cap + e];
+                dst.attr[off + e] = src.attr[e];
+            }
+        }
+    };
+
+    for (int k = 0; k < K; ++k) {
+        lane = threadIdx.x & 63;
+        asm volatile("" : "+v"(lane));
+        // (the hand-off's granules are loaded where they are used: published
+        // steps earlier, they normally land without a wait, and held across
+        // the assignment they would cost the 64-VGPR budget scratch spills)
+        // _set_action + apply_environment_force + integrate_state (App. A S3-S6)
+        float Fx = 0.0f, Fy = 0.0f;
+        if (lane < s.N) {
+            const float2 u = roll_action_force(late_params(), arow, eb * Nmax + lane);
+            Fx = u.x;
+            Fy = u.y;
+        }
+        for (int c = 0; c < s.M; ++c) {
+            const float2 q = rl_f2(cp, c);
+            const float dx = cp.x - q.x, dy = cp.y - q.y;
+            const float d2 = dx * dx + dy * dy;
+            const bool ag = c < s.N;
+            if (lane < s.N && c != lane && d2 > 0.0f && d2 < (ag ? P().cut2_aa : P().cut2_ao)) {
+                const float f = contact_scale(P(), d2, ag ? P().dmin_aa : P().dmin_ao);
+                Fx += f * dx;
+                Fy += f * dy;
+            }
+        }
+        if (P().strict) {
+            const bool bad = strict_bad(lane, cp, s.N, s.M, [&](int c) { return rl_f2(cp, c); });
+            if (lane < s.N && bad) {
+                Fx = __builtin_nanf("");
+                Fy = __builtin_nanf("");
+            }
+        }
+        if (lane < s.N) {
+            v.x = v.x * P().omd;
+            v.y = v.y * P().omd;
+            v.x = v.x + (Fx / P().mass) * P().dt;
+            v.y = v.y + (Fy / P().mass) * P().dt;
+            if (P().max_speed > 0.0f) {
+                const float sp = sqrtf(v.x * v.x + v.y * v.y);
+                if (sp > P().max_speed) {
+                    v.x = v.x / sp * P().max_speed;
+                    v.y = v.y / sp * P().max_speed;
+                }
+            }
+            cp.x = cp.x + v.x * P().dt;
+            cp.y = cp.y + v.y * P().dt;
+        }
+        t += 1;
+        const bool done = live && t >= P().EL;
+        // a group's last wave: the group sum of step k - 1
+        if (k >= 1 && glast) xfer_grp_publish(xf(), xfer_grp_load(xf(), k - 1, w, lane), k - 1, w, lane, cur_edges);
+
+        int cnt = 0;
+        rmask = pair_sweep(&cnt);
+        if (lane >= s.N) cnt = 0;
+        const bool will_reset = done && P().auto_reset;
+        if (!will_reset) publish(k);   // ahead of the assignment
+
+        // reward: navigation -|p_i - g_i|; polygon/line -C[i][sigma_i]
+        float2 slot = make_float2(0.0f, 0.0f);
+        int sigma = -1;
+        float r = 0.0f;
+        auto assign = [&]() {
+            slot = slot_of(P(), s, lane, tp);
+            float own;
+            KernargParams &q = late_params();
+            const LsaWarm lw{q.lsa_v ? q.lsa_v + eb * Nmax : nullptr, q.lsa_col ? q.lsa_col + eb * Nmax : nullptr,
+                             q.lsa_stats ? q.lsa_stats + 2 * eb : nullptr};
+            // the lane state the assignment does not read waits in LDS (the
+            // 64-VGPR budget: held in registers it would spill to scratch)
+            // (agents and targets sit in lanes < 32: N_max <= 32; lanes past
+            // them hold zeros)
+            if (lane < kRaggedMaxAgents) s_stash[lane] = make_float4(v.x, v.y, tp.x, tp.y);
+            s_rm[lane] = rmask;
+            sigma = wave_lsa<true>(s.N, lane, cp, slot, s_lsa, &own, lw);
+            const float4 st = lane < kRaggedMaxAgents ? s_stash[lane] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            v = make_float2(st.x, st.y);
+            tp = make_float2(st.z, st.w);
+            rmask = s_rm[lane];
+            return own;
+        };
+        if (s.scn == kScnNav) {
+            if (lane < s.N) {
+                const float dx = cp.x - tp.x, dy = cp.y - tp.y;
+                r = -sqrtf(dx * dx + dy * dy);
+            }
+        } else {
+            r = -assign();
+        }
+        float rsum = wave_sum(lane < s.N ? r : 0.0f);
+        if (P().shared_reward) {
+            r = rsum;
+            rsum *= (float)s.N;
+        }
+        {
+            KernargParams &q = late_params();
+            if (lane < Nmax) {
+                (q.ro.rew + (kSlots ? k * q.ro.rc_s : 0))[eb * Nmax + lane] = lane < s.N ? r : 0.0f;
+                (q.ro.cost + (kSlots ? k * q.ro.rc_s : 0))[eb * Nmax + lane] = (float)cnt;
+            }
+        }
+        const int csum = wave_sum(cnt);
+        acc.x += rsum;
+        acc.y += (float)csum;
+        bool relaid = false;
+        if (will_reset) {
+            // auto-reset: scenario.reset_world (as ragged_env_step's relayout),
+            // then the observation of the new layout
+            if (lane == 0) late_params().ep_last[eb] = acc;
+            ep = ep + 1;
+            t = 0;
+            acc = make_float2(0.0f, 0.0f);
+            s = draw_shape(P(), w);
+            const uint32_t gid = (uint32_t)(P().env_base + w);
+            cp = make_float2(0.0f, 0.0f);
+            tp = cp;
+            v = cp;
+            if (lane < s.M) cp = layout_at(P(), s, gid, (uint32_t)ep, lane < s.N ? lane : s.N + s.T + (lane - s.N));
+            if (lane < s.T) tp = layout_at(P(), s, gid, (uint32_t)ep, s.N + lane);
+            relaid = relaid_any = true;
+            rmask = pair_sweep(&cnt);
+            if (s.scn != kScnNav) (void)assign();
+            publish(k);
+        }
+
+        // node features [v, p, target - p, type]; target = own goal / assigned slot
+        const bool full_nf = relaid || P().nf_full;
+        float2 tgt = tp;
+        if (s.scn != kScnNav) {
+            const int src = sigma < 0 ? 0 : sigma;
+            tgt = make_float2(__shfl(slot.x, src), __shfl(slot.y, src));
+        }
+        KernargParams &q = late_params();
+        float *const nfb = q.ro.nf + (kSlots ? k * q.ro.nf_s : 0) + eb * Emax * 7;
+        if (live && lane < s.N) {
+            float *nf = nfb + lane * 7;
+            nf[0] = v.x;
+            nf[1] = v.y;
+            nf[2] = cp.x;
+            nf[3] = cp.y;
+            nf[4] = tgt.x - cp.x;
+            nf[5] = tgt.y - cp.y;
+            if (full_nf) nf[6] = 0.0f;
+        }
+        if (live && lane < Nmax) {
+            int32_t *const asg = q.ro.asg + (kSlots ? k * q.ro.as_s : 0);
+            asg[eb * Nmax + lane] = (lane < s.N && s.scn != kScnNav) ? sigma : -1;
+        }
+        if (live && full_nf) {
+            // the static rows of every storage row (padding: 0, type -1)
+            for (int qq = lane; qq < Emax; qq += kWave) s_pos[qq] = make_float2(0.0f, 0.0f);
+            wave_sync();
+            if (lane < s.M) s_pos[collider_row(P(), s, lane)] = cp;
+            if (lane < s.T) s_pos[Nmax + lane] = tp;
+            wave_sync();
+            for (int qq = lane; qq < Emax; qq += kWave) {
+                if (qq < s.N) continue;   // live agent rows written above
+                const float2 pq = s_pos[qq];
+                float type;
+                if (qq < Nmax) type = -1.0f;
+                else if (qq < Nmax + Tmax) type = qq - Nmax < s.T ? 1.0f : -1.0f;
+                else type = qq - Nmax - Tmax < s.O ? 2.0f : -1.0f;
+                float *nf = nfb + qq * 7;
+                nf[0] = 0.0f;
+                nf[1] = 0.0f;
+                nf[2] = pq.x;
+                nf[3] = pq.y;
+                nf[4] = 0.0f;
+                nf[5] = 0.0f;
+                nf[6] = type;
+            }
+            wave_sync();
+        }
+        if (live && lane == 0) {
+            (q.ro.done + (kSlots ? k * q.ro.done_s : 0))[eb] = done ? 1 : 0;
+            if (kSlots || k == K - 1) (q.ro.ecount + (kSlots ? k * q.ro.ec_s : 0))[eb] = cur_edges;
+        }
+        if (k == K - 1 && q.degenerate && lane == 0) {}   // flags written with the final state
+        // the edges of step k - depth
+        if (k >= D) pack(k - D, xfer_off_settle(xf(), xfer_off_load(xf(), k - D, w, lane), k - D, w, lane));
+        arow = arow + 1 == n_act ? 0 : arow + 1;
+        ring = ring == D ? 0 : ring + 1;
+    }
+    // ---- the tail: the last group sums, the last `depth` steps' edges, the
+    // last step's edge sums per env block (later eager emit launches)
+    for (int k = K; k < K + D; ++k) {
+        XferOff xo{0u, 0u, 0u};
+        uint32_t xl = 0;
+        if (k >= D) xo = xfer_off_load(xf(), k - D, w, lane);
+        if (k == K) {
+            if (glast) xl = xfer_grp_load(xf(), K - 1, w, lane);
+            // block_edge_sum of env block w / 4: its last env adds the others' counts
+            const int cfirst = w & ~(kWavesPerBlock - 1);
+            if (w == min(cfirst + kWavesPerBlock, P().B) - 1) {
+                const Xfer x = xf();
+                const uint32_t *g = x.agg + (int64_t)(K - 1) * x.W + cfirst + min(lane, max(w - cfirst - 1, 0));
+                const uint32_t cv = xfer_settle(xfer_ld(g), g, lane < w - cfirst, x.tag(K - 1), x.status);
+                const int tot = wave_total((int)cv) + cur_edges;
+                if (lane == 0) late_params().block_edge_sum[w / kWavesPerBlock] = tot;
+            }
+            if (glast) xfer_grp_publish(xf(), xl, K - 1, w, lane, cur_edges);
+        }
+        if (k >= D) pack(k - D, xfer_off_settle(xf(), xo, k - D, w, lane));
+        ring = ring == D ? 0 : ring + 1;
+    }
+    // The grid's last wave has read (directly or through the group sums) a
+    // granule of this launch from every wave: advance the epoch.
+    if (w == xf().W - 1 && lane == 0) {
+        KernargParams &q = late_params();
+        __hip_atomic_store((gu32 *)q.roll.epoch, ((xbase / (uint32_t)K) + 1u) & 0xffffu, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // ---- the final state (what the next launch or an eager step reads)
+    if (!live) return;
+    KernargParams &q = late_params();
+    float2 *const pos_b = q.pos + eb * Emax;
+    if (relaid_any) {   // every storage row (padding 0), as a reset writes them
+        for (int qq = lane; qq < Emax; qq += kWave) s_pos[qq] = make_float2(0.0f, 0.0f);
+        wave_sync();
+        if (lane < s.M) s_pos[collider_row(p, s, lane)] = cp;
+        if (lane < s.T) s_pos[Nmax + lane] = tp;
+        wave_sync();
+        for (int qq = lane; qq < Emax; qq += kWave) pos_b[qq] = s_pos[qq];
+        if (lane < Nmax) q.vel[eb * Nmax + lane] = lane < s.N ? v : make_float2(0.0f, 0.0f);
+    } else if (lane < s.N) {
+        pos_b[lane] = cp;
+        q.vel[eb * Nmax + lane] = v;
+    }
+    if (lane < s.M) q.row_mask[eb * p.M + lane] = rmask;
+    const bool nonfin = __any(lane < s.N && nonfinite2(cp));
+    if (lane == 0) {
+        if (q.degenerate) q.degenerate[eb] = (uint8_t)((coinc ? kDegCoincident : 0) | (nonfin ? kDegNonfinite : 0));
+        q.step_count[eb] = t;
+        q.episode[eb] = ep;
+        q.ep_acc[eb] = acc;
+        if (relaid_any) q.env_shape[eb] = s.N | (s.scn << 8);
+    }
+}
+
+const void *roll_ragged_kernel_fn(const DevParams &p, bool slots) {
+    if (p.path != kPathRagged) return nullptr;
+    return slots ? reinterpret_cast<const void *>(&gsm_roll_ragged_kernel<true>)
+                 : reinterpret_cast<const void *>(&gsm_roll_ragged_kernel<false>);
+}
+size_t roll_ragged_kernel_lds(const DevParams &p) {
+    return (size_t)kWavesPerBlock * (p.wave_lds_step + kRaggedRollWaveLds);
 }
 
 const void *step_ragged_kernel_fn() { return reinterpret_cast<const void *>(&gsm_step_ragged_kernel<false>); }

@@ -767,26 +767,6 @@ size_t roll_tile_kernel_lds(const DevParams &p) {
            8 * (size_t)p.W * (2 * p.M + p.N);
 }
 
-template <typename Params>
-__device__ __forceinline__ float2 roll_tile_force(const Params &p, int row, int64_t a) {
-    const char *base = p.roll.actions + (int64_t)row * p.roll.stride;
-    float ux, uy;
-    if (p.action_fmt == 0) {
-        const float *q = (const float *)base + a * 5;
-        ux = q[1] - q[2];
-        uy = q[3] - q[4];
-    } else if (p.action_fmt == 1) {
-        const int k = ((const int32_t *)base)[a];
-        ux = (float)(k == 1) - (float)(k == 2);
-        uy = (float)(k == 3) - (float)(k == 4);
-    } else {
-        const float2 q = ((const float2 *)base)[a];
-        ux = q.x;
-        uy = q.y;
-    }
-    return make_float2(ux * p.sens, uy * p.sens);
-}
-
 template <bool kSlots>   // per-step outputs at base + k * stride (a rollout buffer), else in place
 __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -862,7 +842,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         const uint64_t *cm = s_cm;
         for (int i = tid; i < N; i += kTileBlock) {
             const float2 pi = s_pos[i];
-            const float2 u = roll_tile_force(late_params(), arow, eb * N + i);
+            const float2 u = roll_action_force(late_params(), arow, eb * N + i);
             float fx = 0.0f, fy = 0.0f;
             for (int kw = 0; kw < W; ++kw) {
                 uint64_t bits = cm[(int64_t)i * W + kw];

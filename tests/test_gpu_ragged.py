@@ -224,8 +224,8 @@ def test_lagged_chain_equals_eager(scenario, N, B, T):
 
 
 def test_lagged_chain_every_step_into_rollout_slots():
-    """capture_into on a mixed config: the lagged chain writes slot j's edges
-    from step j+1's kernel; every slot equals eager step_into's."""
+    """capture_into on a mixed config (one ragged rollout launch, slot j's
+    edges packed `depth` steps later): every slot equals eager step_into's."""
     from gsmarl_amd import EnvConfig, GpuBatchEnv, GraphRolloutBuffer
     B, N, T = 300, 24, 7
     kw = dict(scenario="mixed", n_agents=N, n_envs=B, seed=4, episode_length=4)
@@ -235,7 +235,7 @@ def test_lagged_chain_every_step_into_rollout_slots():
     eb = GraphRolloutBuffer(ref, episode_length=T)
     gb.reset(seed=4)
     gb.capture(acts)
-    assert not env.graph_is_rollout(0)
+    assert env.graph_is_rollout(0)
     gb.replay()
     eb.reset(seed=4)
     for t in range(T):

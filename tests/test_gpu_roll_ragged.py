@@ -1,0 +1,192 @@
+"""Fused rollout of ragged batches (polygon / line / mixed; config C4):
+gsm_roll_ragged_kernel runs all T steps of a graph in one launch, one env per
+wave, each env packing its edges `depth` steps behind its own step through a
+per-env slab. Every state and output buffer must equal the
+eager steps' bit for bit (which test_gpu_ragged checks against the oracle):
+partial workgroups, auto-resets inside the launch, all three action formats,
+pack depths 2..8, repeated replays, rollout-buffer slots (assignments
+included), three full-size C4 episodes against the lagged chain, and the last
+step of a launch against oracle/ragged_ref.py directly."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import ragged_ref as rr
+from parity_tol import check_state
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+KEYS = ("pos", "vel", "step_count", "episode", "node_feat", "reward", "cost", "done", "edge_count",
+        "edge_ptr", "ep_acc", "ep_last", "row_mask", "assign", "env_shape", "lsa_v", "lsa_col", "lsa_stats")
+
+
+def _env(**kw):
+    from gsmarl_amd import EnvConfig, GpuBatchEnv
+    return GpuBatchEnv(EnvConfig(**kw), DEV)
+
+
+def _acts(fmt, T, B, N, gen):
+    if fmt == "index":
+        return torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV, generator=gen)
+    if fmt == "onehot":
+        k = torch.randint(0, 5, (T, B, N), device=DEV, generator=gen)
+        return torch.nn.functional.one_hot(k, 5).to(torch.float32)
+    return torch.rand((T, B, N, 2), device=DEV, generator=gen) * 2 - 1
+
+
+def _same(ref, env, what):
+    for k in KEYS:
+        assert torch.equal(ref[k], env.t[k]), (what, k)
+    n = int(ref["edge_ptr"][-1])
+    assert torch.equal(ref["edge_index"][:, :n], env.t["edge_index"][:, :n]), what
+    assert torch.equal(ref["edge_attr"][:n], env.t["edge_attr"][:n]), what
+
+
+@pytest.fixture
+def depth(request):
+    old = os.environ.get("GSM_ROLL_DEPTH")
+    if request.param is not None:
+        os.environ["GSM_ROLL_DEPTH"] = str(request.param)
+    yield request.param
+    if old is None:
+        os.environ.pop("GSM_ROLL_DEPTH", None)
+    else:
+        os.environ["GSM_ROLL_DEPTH"] = old
+
+
+@pytest.mark.parametrize("depth,scenario,N,B,T,EL,fmt", [
+    (None, "mixed", 24, 257, 9, 3, "index"), (None, "mixed", 24, 64, 2, 5, "index"),
+    (None, "mixed", 24, 40, 1, 5, "index"), (None, "polygon", 12, 130, 7, 4, "onehot"),
+    (None, "line", 9, 64, 5, 3, "cont"), (None, "mixed", 24, 8192, 12, 5, "index"),
+    (2, "mixed", 24, 300, 11, 4, "index"), (8, "mixed", 24, 300, 11, 4, "index"), (8, "polygon", 24, 100, 3, 2, "index"),
+], indirect=["depth"])
+def test_roll_ragged_equals_eager(depth, scenario, N, B, T, EL, fmt):
+    env = _env(scenario=scenario, n_agents=N, n_envs=B, seed=7, episode_length=EL)
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(B + T)
+    acts = _acts(fmt, max(T - 2, 1), B, N, gen)   # fewer action rows than steps: the ring wraps
+    env.reset(seed=7)
+    for t in range(2 * T):
+        env.step(acts[t % acts.shape[0]], sync_edges=False)
+        if t == T - 1:
+            torch.cuda.synchronize()
+            ref1 = {k: v.clone() for k, v in env.t.items()}
+    torch.cuda.synchronize()
+    ref2 = {k: v.clone() for k, v in env.t.items()}
+    env.reset(seed=7)
+    env.t["lsa_stats"].zero_()
+    env.capture(acts, T, slot=0, kernels="roll")
+    assert env.graph_is_rollout(0)
+    env.t["edge_index"].fill_(-7)
+    env.replay(0)
+    torch.cuda.synchronize()
+    assert not env.roll_gave_up()
+    ref1["lsa_stats"] = env.t["lsa_stats"].clone()   # counters: compared through the assignments
+    _same(ref1, env, "roll")
+    env.replay(0)   # a second replay continues from the state (granules of a new epoch)
+    torch.cuda.synchronize()
+    assert not env.roll_gave_up()
+    ref2["lsa_stats"] = env.t["lsa_stats"].clone()
+    _same(ref2, env, "roll x2")
+    env.close()
+
+
+def test_roll_ragged_episodes_match_chain():
+    """C4 at full size (mixed N in {3..24} x 8192): three 100-step episodes
+    replayed back to back as rollout launches leave every buffer exactly as
+    the lagged per-step chain does."""
+    B, N, T = 8192, 24, 100
+    env = _env(scenario="mixed", n_agents=N, n_envs=B, n_agents_min=3, seed=5, episode_length=T)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    env.reset(seed=5)
+    env.capture(acts, T, slot=0, kernels="both")
+    for _ in range(3):
+        env.replay(0)
+    torch.cuda.synchronize()
+    ref = {k: v.clone() for k, v in env.t.items()}
+    env.reset(seed=5)
+    env.t["lsa_stats"].zero_()
+    env.capture(acts, T, slot=1, kernels="roll")
+    assert env.graph_is_rollout(1)
+    for _ in range(3):
+        env.replay(1)
+    torch.cuda.synchronize()
+    assert not env.roll_gave_up()
+    ref["lsa_stats"] = env.t["lsa_stats"].clone()
+    _same(ref, env, "3 episodes")
+    env.close()
+
+
+@pytest.mark.parametrize("scenario,N,B", [("mixed", 24, 96), ("polygon", 10, 40), ("line", 7, 40)])
+def test_roll_ragged_last_step_oracle(scenario, N, B):
+    """The last step of a rollout launch vs oracle/ragged_ref.py stepped from
+    the identical fp32 state before it (eager steps reach that state bit for
+    bit): positions / velocities within the 1e-6 bar, edges, assignments,
+    costs and node features exact. Episode length 4 puts auto-resets inside
+    the launch."""
+    from gsmarl_amd import EnvConfig
+    T = 9
+    cfg = EnvConfig(scenario=scenario, n_agents=N, n_envs=B, seed=21, episode_length=4)
+    keys = set(rr.br.DEFAULTS) | set(rr.RAGGED_DEFAULTS)
+    rcfg = rr.make_cfg(**{k: v for k, v in cfg.to_dict().items() if k in keys})
+    env = _env(**cfg.to_dict())
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    env.reset(seed=21)
+    for t in range(T - 1):
+        env.step(acts[t], sync_edges=False)
+    torch.cuda.synchronize()
+    sh = env.t["env_shape"].cpu().numpy()
+    st = dict(pos=env.t["pos"].cpu().numpy(), vel=env.t["vel"].cpu().numpy(),
+              step=env.t["step_count"].cpu().numpy().copy(), episode=env.t["episode"].cpu().numpy().copy(),
+              ep_acc=env.t["ep_acc"].cpu().numpy().astype(np.float64),
+              ep_last=env.t["ep_last"].cpu().numpy().astype(np.float64), n=sh & 0xFF, scn=sh >> 8, seed=21)
+    nst, _ = rr.step(rcfg, st, acts[T - 1].cpu().numpy(), 1, np.float64)
+    env.reset(seed=21)
+    env.capture(acts, T, slot=0, kernels="roll")
+    env.replay(0)
+    torch.cuda.synchronize()
+    assert not env.roll_gave_up()
+    check_state(env.t["pos"].cpu().numpy(), nst["pos"], f"pos roll {scenario}")
+    check_state(env.t["vel"].cpu().numpy(), nst["vel"], f"vel roll {scenario}")
+    assert np.array_equal(env.t["step_count"].cpu().numpy(), nst["step"])
+    assert np.array_equal(env.t["episode"].cpu().numpy(), nst["episode"])
+    ob32 = rr.observe(rcfg, dict(st, pos=env.t["pos"].cpu().numpy(), vel=env.t["vel"].cpu().numpy(),
+                                 step=nst["step"], episode=nst["episode"]))
+    assert np.array_equal(env.t["edge_ptr"].cpu().numpy(), ob32["edge_ptr"])
+    n = int(ob32["edge_ptr"][-1])
+    assert np.array_equal(env.t["edge_index"][:, :n].cpu().numpy(), ob32["edge_index"])
+    assert np.array_equal(env.t["assign"].cpu().numpy(), ob32["assign"])
+    assert np.array_equal(env.t["node_feat"].cpu().numpy(), ob32["node_feat"])
+    env.close()
+
+
+def test_roll_ragged_into_buffer_slots():
+    """capture_into on a mixed batch is one rollout launch writing slot j's
+    outputs (assignments included; edges packed into slot j `depth` steps
+    later); every slot equals eager step_into's."""
+    from gsmarl_amd import EnvConfig, GpuBatchEnv, GraphRolloutBuffer
+    B, N, T = 300, 24, 9
+    kw = dict(scenario="mixed", n_agents=N, n_envs=B, seed=4, episode_length=4)
+    env, ref = GpuBatchEnv(EnvConfig(**kw), DEV), GpuBatchEnv(EnvConfig(**kw), DEV)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    gb, eb = GraphRolloutBuffer(env, episode_length=T), GraphRolloutBuffer(ref, episode_length=T)
+    gb.reset(seed=4)
+    gb.capture(acts)
+    assert env.graph_is_rollout(0)
+    gb.replay()
+    gb.validate()
+    eb.reset(seed=4)
+    for t in range(T):
+        eb.insert(acts[t])
+    torch.cuda.synchronize()
+    for k in ("node_feat", "reward", "cost", "done", "edge_ptr", "edge_count", "assign"):
+        assert torch.equal(getattr(gb, k), getattr(eb, k)), k
+    for t in range(T + 1):
+        n = int(gb.edge_ptr[t, B])
+        assert torch.equal(gb.edge_index[t][:, :n], eb.edge_index[t][:, :n]), t
+        assert torch.equal(gb.edge_attr[t][:n], eb.edge_attr[t][:n]), t
+    env.close()
+    ref.close()
