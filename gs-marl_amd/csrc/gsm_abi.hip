@@ -659,13 +659,11 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: the batch exceeds one residency round of the rollout kernel");
     }
     const int K = n_steps;
-    // tags carry the step in 12 bits (ragged: per-wave granules) or 16
-    // (look-back granules); checked before the slot's graph is dropped
-    const int max_k = ragged ? gsm::kXferMaxSteps : 65535;
-    if (K > max_k) {
+    // granule tags carry the step in 12 bits; checked before the slot's
+    // graph is dropped
+    if (K > gsm::kRollMaxSteps) {
         if (fallback) return kRollIneligible;
-        return fail(h, GSM_EINVAL, ragged ? "GSM_GRAPH_ROLL: n_steps must be <= 4095"
-                                          : "GSM_GRAPH_ROLL: n_steps must be <= 65535");
+        return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: n_steps must be <= 4095");
     }
     // ragged: per-wave granules, groups of 64 waves (at most 128 groups: one
     // residency round holds <= 8192 waves), edges packed `depth` steps late
@@ -715,23 +713,28 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     }
     gsm_handle::Slot &sl = h->slots[slot];
     drop_slot(sl);
-    // a 16-byte header (the launch epoch), then ragged: per-wave counts
-    // [K][xW] and group sums [K][xNG] (32-bit granules); segmented / tile:
+    // a 16-byte header (the launch epoch), then 8-byte granules. Ragged:
+    // per-wave counts [K][xW] and group sums [K][xNG]; segmented / tile:
     // aggregates [K][nb] and inclusive prefixes [K][nb] (look-back). Zeroed
     // once here — granules are tagged with the launch epoch, so replays never
     // clear them
-    const size_t gran_alloc = ragged ? 16 + (size_t)K * (xW + xNG) * sizeof(uint32_t)
-                                     : 16 + 2 * (size_t)K * nb * sizeof(uint64_t);
+    const size_t gran_alloc = 16 + (size_t)K * (ragged ? (size_t)(xW + xNG) : 2 * (size_t)nb) * sizeof(uint64_t);
     e = hipMalloc(&sl.gran, gran_alloc);
     if (e != hipSuccess) {
         sl.gran = nullptr;
         if (fallback) return kRollIneligible;   // the per-step chain needs no granules
         return hip_fail(h, e, "hipMalloc (rollout granules)");
     }
-    // every capture starts its granules at a new epoch (process-wide counter),
-    // written, like the zeros, by agent-scope stores (launch_granule_init)
-    static std::atomic<uint32_t> next_epoch{0};
-    e = gsm::launch_granule_init(sl.gran, gran_alloc, next_epoch.fetch_add(1) & 0xffffu, h->cap_stream);
+    // Every capture starts at a fresh block of 4096 launch epochs (20-bit
+    // epochs: 256 blocks before the counter wraps). A memset or store-zeroed
+    // allocation was seen to still show an agent-scope load granules left at
+    // that address by a freed graph's last replay; with consecutive start
+    // epochs those carried this graph's first tags (a freed graph replayed
+    // twice had used epochs e, e + 1; the next capture started at e + 1). No
+    // graph replayed fewer than 4096 times shares an epoch with another.
+    static std::atomic<uint32_t> next_block{0};
+    const uint32_t epoch0 = (next_block.fetch_add(1) * 4096u + 1u) & 0xfffffu;
+    e = gsm::launch_granule_init(sl.gran, gran_alloc, epoch0, h->cap_stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->cap_stream);
     if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "rollout granule init"); }
     const bool ends = (flags & GSM_GRAPH_TIME_ENDS) != 0;

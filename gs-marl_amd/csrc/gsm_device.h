@@ -257,56 +257,62 @@ __device__ __forceinline__ float2 roll_action_force(const Params &p, int row, in
     return make_float2(ux * p.sens, uy * p.sens);
 }
 
+// ---- granule tags of the rollouts' CSR hand-offs
+// A granule is 8 bytes {tag32 << 32 | value32}, stored and loaded with relaxed
+// agent-scope atomics (write-through, no fence). tag32 = epoch20 << 12 |
+// (step + 1): the launch epoch (20 bits; read from the graph's epoch word at
+// launch start, advanced in-kernel once every wave / workgroup has read it)
+// and the step within the launch (K <= kRollMaxSteps). Every capture starts
+// at a fresh block of 4096 epochs (gsm_abi.hip), so no granule left in memory
+// by an earlier launch — of this graph, or of a graph freed before this one
+// was allocated at the same address — carries a tag of this launch (observed
+// otherwise: a memset / store-initialised allocation still showed an
+// agent-scope load the granules of the previous graph's last replay). Tag 0
+// is never valid (step + 1 >= 1), so zeroed memory never matches.
+__device__ __forceinline__ uint32_t roll_epoch_tag(uint32_t epoch) { return (epoch & 0xfffffu) << 12; }
+__device__ __forceinline__ uint32_t roll_next_epoch(uint32_t epoch) { return (epoch + 1u) & 0xfffffu; }
+
 // ---- per-wave CSR hand-off of the one-env-per-wave rollouts
-//
 // (the ragged rollout, gsm_ragged_kernels.hip; `depth` = the lag between a
 // step and the packing of its edges, >= 2). The packed CSR offset of env (=
 // wave) w at step s is the sum of the edge counts of every wave before it.
-// Three levels, all 32-bit granules
-// {tag12 << 20 | value20} stored and loaded with relaxed agent-scope atomics
-// (write-through, no fence):
+// Three levels of tagged granules:
 //   agg[s][w]  wave w's edge count at step s, published right after its sweep;
 //   grp[s][g]  the sum of agg[s][64g .. 64g+63], published by wave 64g+63 in
-//              iteration s + 1 (its loads issued at the top of that iteration);
+//              iteration s + 1;
 //   offset     sum of grp[s][g' < w/64] + sum of agg[s][64(w/64) .. w-1],
-//              loaded at the top of iteration s + depth and summed at its
-//              end, when step s's edges are packed.
+//              loaded and summed in iteration s + depth, when step s's edges
+//              are packed.
 // Every granule a wave reads was published at least one iteration before it
-// is needed, so the loads' latency hides behind a whole step and no wave waits
-// in the normal case; there are no barriers. A wave waits only on waves of
-// lower index (dispatched before it), so the launch always progresses; every
-// wait is bounded (kRollSpinTicks, then a sticky status word). Tag of step s:
-// (epoch * K + s + 1) mod 4096 with the launch epoch read at launch start and
-// advanced by the grid's last wave once it has (transitively) read every
-// wave's last granule; a granule left by the previous launch differs by
-// K mod 4096 != 0 (K <= 4095), and every granule is rewritten every launch, so
-// none is ever cleared.
-constexpr uint32_t kXferTagMask = 0xfffu, kXferValMask = (1u << 20) - 1u;   // K <= kXferMaxSteps
+// is needed, so no wave normally waits; there are no barriers. A wave waits
+// only on waves of lower index (dispatched before it), so the launch always
+// progresses; every wait is bounded (kRollSpinTicks, then a sticky status
+// word).
 struct Xfer {
-    uint32_t *agg;      // [K][W]
-    uint32_t *grp;      // [K][NG]
+    uint64_t *agg;      // [K][W]
+    uint64_t *grp;      // [K][NG]
     uint32_t *status;
     int W, NG;          // waves of the grid, groups of 64 waves
-    uint32_t base;      // epoch * K (mod 4096 in the tags)
-    __device__ __forceinline__ uint32_t tag(int s) const { return (base + (uint32_t)s + 1u) & kXferTagMask; }
+    uint32_t etag;      // roll_epoch_tag(epoch)
+    __device__ __forceinline__ uint32_t tag(int s) const { return etag | (uint32_t)(s + 1); }
 };
-__device__ __forceinline__ uint32_t xfer_ld(const uint32_t *g) {
-    return __hip_atomic_load((const gu32 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ uint64_t xfer_ld(const uint64_t *g) {
+    return __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void xfer_st(uint32_t *g, uint32_t tag, uint32_t v) {
-    __hip_atomic_store((gu32 *)g, tag << 20 | (v & kXferValMask), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ void xfer_st(uint64_t *g, uint32_t tag, uint32_t v) {
+    __hip_atomic_store((gu64 *)g, (uint64_t)tag << 32 | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // The value of a granule loaded as x from g on lanes `act`, once its tag is
 // `tag` (re-polled until it is: the cold path); 0 on other lanes.
-__device__ __forceinline__ uint32_t xfer_settle(uint32_t x, const uint32_t *g, bool act, uint32_t tag,
+__device__ __forceinline__ uint32_t xfer_settle(uint64_t x, const uint64_t *g, bool act, uint32_t tag,
                                                 uint32_t *status) {
-    bool bad = act && (x >> 20) != tag;
+    bool bad = act && (uint32_t)(x >> 32) != tag;
     if (__builtin_expect(__builtin_amdgcn_ballot_w64(bad) != 0, 0)) {
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         do {
             __builtin_amdgcn_s_sleep(2);
             if (bad) x = xfer_ld(g);
-            bad = act && (x >> 20) != tag;
+            bad = act && (uint32_t)(x >> 32) != tag;
             if (__builtin_amdgcn_s_memrealtime() - t0 > kRollSpinTicks ||
                 __hip_atomic_load((gu32 *)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
                 __hip_atomic_store((gu32 *)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -314,40 +320,40 @@ __device__ __forceinline__ uint32_t xfer_settle(uint32_t x, const uint32_t *g, b
             }
         } while (__builtin_amdgcn_ballot_w64(bad) != 0);
     }
-    return act ? (x & kXferValMask) : 0u;
+    return act ? (uint32_t)x : 0u;
 }
 // Granules wave w needs for step s's offset, loaded at clamped (always valid)
 // addresses with the lane predicates applied when they are settled.
 struct XferOff {
-    uint32_t a, g0, g1;
+    uint64_t a, g0, g1;
 };
 __device__ __forceinline__ XferOff xfer_off_load(const Xfer &x, int s, int w, int lane) {
     const int g = w >> 6, r = w & 63;
-    const uint32_t *ag = x.agg + (int64_t)s * x.W + (g << 6);
-    const uint32_t *gg = x.grp + (int64_t)s * x.NG;
+    const uint64_t *ag = x.agg + (int64_t)s * x.W + (g << 6);
+    const uint64_t *gg = x.grp + (int64_t)s * x.NG;
     const int gl = g > 0 ? g - 1 : 0;
     XferOff o;
     o.a = xfer_ld(ag + min(lane, r > 0 ? r - 1 : 0));
     o.g0 = xfer_ld(gg + min(lane, gl));
-    o.g1 = g > kWave ? xfer_ld(gg + min(lane + kWave, gl)) : 0u;   // wave-uniform branch
+    o.g1 = g > kWave ? xfer_ld(gg + min(lane + kWave, gl)) : 0ull;   // wave-uniform branch
     return o;
 }
 __device__ __forceinline__ int xfer_off_settle(const Xfer &x, const XferOff &o, int s, int w, int lane) {
     const int g = w >> 6, r = w & 63, gl = g > 0 ? g - 1 : 0;
     const uint32_t tag = x.tag(s);
-    const uint32_t *ag = x.agg + (int64_t)s * x.W + (g << 6);
-    const uint32_t *gg = x.grp + (int64_t)s * x.NG;
+    const uint64_t *ag = x.agg + (int64_t)s * x.W + (g << 6);
+    const uint64_t *gg = x.grp + (int64_t)s * x.NG;
     uint32_t v = xfer_settle(o.a, ag + min(lane, r > 0 ? r - 1 : 0), lane < r, tag, x.status);
     v += xfer_settle(o.g0, gg + min(lane, gl), lane < g, tag, x.status);
     if (g > kWave) v += xfer_settle(o.g1, gg + min(lane + kWave, gl), lane + kWave < g, tag, x.status);
     return wave_total((int)v);
 }
 // Group sum of step s by the group's last wave (w & 63 == 63): the other 63
-// members' granules (loaded at the top of iteration s + 1) plus its own count.
-__device__ __forceinline__ uint32_t xfer_grp_load(const Xfer &x, int s, int w, int lane) {
+// members' granules plus its own count.
+__device__ __forceinline__ uint64_t xfer_grp_load(const Xfer &x, int s, int w, int lane) {
     return xfer_ld(x.agg + (int64_t)s * x.W + (w & ~63) + min(lane, 62));
 }
-__device__ __forceinline__ void xfer_grp_publish(const Xfer &x, uint32_t l, int s, int w, int lane, int own) {
+__device__ __forceinline__ void xfer_grp_publish(const Xfer &x, uint64_t l, int s, int w, int lane, int own) {
     const uint32_t tag = x.tag(s);
     const uint32_t v = xfer_settle(l, x.agg + (int64_t)s * x.W + (w & ~63) + min(lane, 62), lane < 63, tag, x.status);
     const int sum = wave_total((int)v) + own;

@@ -24,8 +24,9 @@ __host__ __device__ constexpr int lsa_lds_bytes(int nmax) {
 // cap on envs per wave, keeping a block's envs (4G) within one wave's lanes
 // (C2, 3 x 4096: G = 4 runs 6.0 us per step against 6.9 at G = 10)
 constexpr int kMaxSegEnvsPerWave = 4;
-// steps of a one-env-per-wave rollout launch (12-bit granule tags, gsm_device.h Xfer)
-constexpr int kXferMaxSteps = 4095;
+// steps of one rollout launch (the step field of the 32-bit granule tags,
+// gsm_device.h roll_epoch_tag)
+constexpr int kRollMaxSteps = 4095;
 
 // Everything a launch needs, passed by value (kernarg segment, < 4 KB).
 // fp32 constants are formed on the host exactly as oracle/batch_ref.py:Spec
@@ -90,13 +91,14 @@ struct DevParams {
     // actions at actions + ((t_first + k) % n_actions) * stride and emits the
     // edges of an earlier step (ro); the tail after the loop emits the last.
     // The CSR prefix of step t crosses waves / workgroups through `gran`,
-    // after a 16-byte header holding the launch epoch: one-env-per-wave
-    // rollouts use 32-bit per-wave granules and group sums (gsm_device.h Xfer,
-    // emission two steps behind); the tile rollout 8-byte {tag, env edge sum}
-    // granules, aggregates [K][grid] then inclusive prefixes [K][grid]
-    // (decoupled look-back, tag = epoch << 16 | (k + 1)). The epoch is
-    // advanced by the launch's last wave / workgroup once every one has read
-    // it, so no granule is ever cleared between launches. `status` is set when
+    // after a 16-byte header holding the launch epoch. Granules are 8-byte
+    // {tag32, value32} (gsm_device.h roll_epoch_tag: 20-bit epoch, 12-bit
+    // step): the ragged rollout's per-wave counts and group sums (Xfer,
+    // packing `depth` steps behind), the seg / tile rollouts' workgroup
+    // aggregates [K][grid] then inclusive prefixes [K][grid] (decoupled
+    // look-back). The epoch is advanced by the launch's last wave / workgroup
+    // once every one has read it, so no granule is ever cleared between
+    // launches; each capture starts at a fresh block of 4096 epochs. `status` is set when
     // a bounded wait gave up.
     struct Roll {
         const char *actions;

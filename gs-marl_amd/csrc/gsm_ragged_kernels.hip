@@ -1101,16 +1101,16 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         if (lane < s.T) tp = pos_b[Nmax + lane];
         if (lane < s.N) v = p.vel[eb * Nmax + lane];
     }
-    const uint32_t xbase = *p.roll.epoch * (uint32_t)K;
+    const uint32_t epoch = *p.roll.epoch;
     auto xf = [&]() -> Xfer {
         KernargParams &q = late_params();
         Xfer x;
         x.W = q.roll.xW;
         x.NG = q.roll.xNG;
-        x.agg = (uint32_t *)(q.roll.gran + 2);
+        x.agg = q.roll.gran + 2;
         x.grp = x.agg + (int64_t)q.roll.K * x.W;
         x.status = q.roll.status;
-        x.base = xbase;
+        x.etag = roll_epoch_tag(epoch);
         return x;
     };
     // launch parameters read at the point of use (late_params): held across
@@ -1285,7 +1285,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         }
         {
             KernargParams &q = late_params();
-            if (lane < Nmax) {
+            if (live && lane < Nmax) {   // (an idle wave's eb aliases env 0)
                 (q.ro.rew + (kSlots ? k * q.ro.rc_s : 0))[eb * Nmax + lane] = lane < s.N ? r : 0.0f;
                 (q.ro.cost + (kSlots ? k * q.ro.rc_s : 0))[eb * Nmax + lane] = (float)cnt;
             }
@@ -1375,8 +1375,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     // ---- the tail: the last group sums, the last `depth` steps' edges, the
     // last step's edge sums per env block (later eager emit launches)
     for (int k = K; k < K + D; ++k) {
-        XferOff xo{0u, 0u, 0u};
-        uint32_t xl = 0;
+        XferOff xo{0ull, 0ull, 0ull};
+        uint64_t xl = 0;
         if (k >= D) xo = xfer_off_load(xf(), k - D, w, lane);
         if (k == K) {
             if (glast) xl = xfer_grp_load(xf(), K - 1, w, lane);
@@ -1384,7 +1384,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             const int cfirst = w & ~(kWavesPerBlock - 1);
             if (w == min(cfirst + kWavesPerBlock, P().B) - 1) {
                 const Xfer x = xf();
-                const uint32_t *g = x.agg + (int64_t)(K - 1) * x.W + cfirst + min(lane, max(w - cfirst - 1, 0));
+                const uint64_t *g = x.agg + (int64_t)(K - 1) * x.W + cfirst + min(lane, max(w - cfirst - 1, 0));
                 const uint32_t cv = xfer_settle(xfer_ld(g), g, lane < w - cfirst, x.tag(K - 1), x.status);
                 const int tot = wave_total((int)cv) + cur_edges;
                 if (lane == 0) late_params().block_edge_sum[w / kWavesPerBlock] = tot;
@@ -1398,7 +1398,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     // granule of this launch from every wave: advance the epoch.
     if (w == xf().W - 1 && lane == 0) {
         KernargParams &q = late_params();
-        __hip_atomic_store((gu32 *)q.roll.epoch, ((xbase / (uint32_t)K) + 1u) & 0xffffu, __ATOMIC_RELAXED,
+        __hip_atomic_store((gu32 *)q.roll.epoch, roll_next_epoch(epoch), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
     // ---- the final state (what the next launch or an eager step reads)

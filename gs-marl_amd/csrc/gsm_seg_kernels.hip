@@ -1078,7 +1078,7 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
 // cost, auto-reset and every store of step t exactly as gsm_step_seg_kernel
 // (same operations in the same order: bit-identical outputs); the
 // workgroup's edge sum of step t is published as an 8-byte {tag, sum}
-// granule (tag = epoch << 16 | (k + 1); one relaxed agent-scope store:
+// granule (tag = roll_epoch_tag(epoch) | (k + 1); one relaxed agent-scope store:
 // write-through, no fence); then the edges of step t - 1 are emitted from the
 // positions and row masks kept from the previous iteration, at the CSR offset
 // found by a decoupled look-back over the preceding workgroups' granules
@@ -1173,7 +1173,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     wave_sync();
 
     const int K = p.roll.K, n_act = p.roll.n_actions;
-    const uint32_t etag = *p.roll.epoch << 16;              // this launch's tag base
+    const uint32_t etag = roll_epoch_tag(*p.roll.epoch);    // this launch's tag base
     int arow = p.roll.t_first % n_act;                      // action row of the current step
     uint8_t deg = 0;                                        // App. A S16 flags of the final state
     // The edges of step t_first + k - 1, emitted in iteration k (k = 1..K-1)
@@ -1202,7 +1202,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
                 // have read the epoch: advance it for the next launch
                 // (granules are never cleared; a stale one cannot match).
                 if (k == K && blockIdx.x == gridDim.x - 1)
-                    __hip_atomic_store((gu32 *)qe.roll.epoch, ((etag >> 16) + 1u) & 0xffffu, __ATOMIC_RELAXED,
+                    __hip_atomic_store((gu32 *)qe.roll.epoch, roll_next_epoch(etag >> 12), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
             }
         }

@@ -267,10 +267,11 @@ int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream);
 #define GSM_GRAPH_TIME_ENDS 8
 #define GSM_GRAPH_UNFUSED 16
 #define GSM_GRAPH_LAG_ONLY 32
-/* GSM_GRAPH_ROLL: all n_steps steps and their edges run in ONE launch
- * (navigation configs with a compiled rollout shape — 3, 6, 12 or 24 agents
- * with as many obstacles, one env per wave — or the tile path, one env per
- * workgroup; the whole batch in one residency round). Each wave keeps its
+/* GSM_GRAPH_ROLL: all n_steps (<= 4095) steps and their edges run in ONE
+ * launch (navigation configs with a compiled rollout shape — 3, 6, 12 or 24
+ * agents with as many obstacles, one env per wave — the tile path, one env
+ * per workgroup, and ragged batches, one env per wave; the whole batch in one
+ * residency round). Each wave keeps its
  * env's state on chip across the steps; workgroups hand the CSR edge-count
  * prefix to each other through tagged granules (bounded waits), and a tail
  * iteration emits the last step's edges. Outputs after the graph are

@@ -219,10 +219,13 @@ def test_roll_episodes_match_chain(N, B):
                                         (24, 300, 2, "bound")])
 def test_roll_recycled_granules(N, B, T, mode):
     """Back-to-back envs of one shape: each capture's granules are a fresh
-    allocation, usually at the address the previous env freed. Its granules
-    are initialised by agent-scope stores at a new epoch, so no granule of the
-    previous allocation is taken for this launch's (a hipMemset's zeros did
-    not hide them: the second env of a pair got the first's group sums)."""
+    allocation, usually at the address the previous env freed, whose granules
+    an agent-scope load may still see after the new allocation is zeroed (a
+    hipMemset's zeros did not hide them: the second env of a pair got the
+    first's group sums). Each graph is replayed three times before it is
+    freed (its in-kernel epoch advances per replay); every capture starts at
+    a fresh block of epochs, so no left-over granule carries a tag of the
+    next graph's launches."""
     from gsmarl_amd import GraphRolloutBuffer
     for rep in range(3):
         env, cfg = _env(n_agents=N, n_envs=B, seed=2, episode_length=6)
@@ -249,5 +252,9 @@ def test_roll_recycled_granules(N, B, T, mode):
             got, want = env.t["edge_ptr"], ref.t["edge_ptr"]
         assert not env.roll_gave_up()
         assert torch.equal(got, want), (rep, (got != want).nonzero().flatten()[:8].tolist())
+        for _ in range(2):   # advance this graph's epoch past the next capture's first
+            gb.replay() if mode == "slots" else env.replay(0)
+        torch.cuda.synchronize()
+        assert not env.roll_gave_up()
         env.close()
         ref.close()

@@ -45,6 +45,15 @@ def _same(ref, env, what):
     assert torch.equal(ref["edge_attr"][:n], env.t["edge_attr"][:n]), what
 
 
+def _fresh(env, seed):
+    """reset(seed) and an empty assignment warm-start cache (the cache is not
+    reset by env.reset: equal runs must start from equal caches)"""
+    env.reset(seed=seed)
+    env.t["lsa_v"].zero_()
+    env.t["lsa_col"].fill_(-1)
+    env.t["lsa_stats"].zero_()
+
+
 @pytest.fixture
 def depth(request):
     old = os.environ.get("GSM_ROLL_DEPTH")
@@ -68,30 +77,56 @@ def test_roll_ragged_equals_eager(depth, scenario, N, B, T, EL, fmt):
     gen = torch.Generator(device=DEV)
     gen.manual_seed(B + T)
     acts = _acts(fmt, max(T - 2, 1), B, N, gen)   # fewer action rows than steps: the ring wraps
-    env.reset(seed=7)
-    for t in range(2 * T):
-        env.step(acts[t % acts.shape[0]], sync_edges=False)
+    _fresh(env, 7)
+    for t in range(2 * T):   # each replay of the graph starts at action row 0
+        env.step(acts[(t % T) % acts.shape[0]], sync_edges=False)
         if t == T - 1:
             torch.cuda.synchronize()
             ref1 = {k: v.clone() for k, v in env.t.items()}
     torch.cuda.synchronize()
     ref2 = {k: v.clone() for k, v in env.t.items()}
-    env.reset(seed=7)
-    env.t["lsa_stats"].zero_()
+    _fresh(env, 7)
     env.capture(acts, T, slot=0, kernels="roll")
     assert env.graph_is_rollout(0)
     env.t["edge_index"].fill_(-7)
     env.replay(0)
     torch.cuda.synchronize()
     assert not env.roll_gave_up()
-    ref1["lsa_stats"] = env.t["lsa_stats"].clone()   # counters: compared through the assignments
     _same(ref1, env, "roll")
     env.replay(0)   # a second replay continues from the state (granules of a new epoch)
     torch.cuda.synchronize()
     assert not env.roll_gave_up()
-    ref2["lsa_stats"] = env.t["lsa_stats"].clone()
     _same(ref2, env, "roll x2")
     env.close()
+
+
+def test_roll_ragged_recycled_granules():
+    """Envs of one shape created back to back (the granules of each capture
+    usually land where the previous env's were freed), each graph replayed
+    three times before it is freed: the next capture's launches never take a
+    left-over granule for theirs (every capture starts at a fresh block of
+    launch epochs; with consecutive start epochs the second graph got the
+    first's second-replay group sums)."""
+    B, N, T = 300, 24, 11
+    for rep in range(3):
+        env = _env(scenario="mixed", n_agents=N, n_envs=B, seed=7, episode_length=4)
+        acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+        _fresh(env, 7)
+        for t in range(T):
+            env.step(acts[t], sync_edges=False)
+        torch.cuda.synchronize()
+        ref = {k: v.clone() for k, v in env.t.items()}
+        _fresh(env, 7)
+        env.capture(acts, T, slot=0, kernels="roll")
+        env.replay(0)
+        torch.cuda.synchronize()
+        assert not env.roll_gave_up()
+        _same(ref, env, f"rep {rep}")
+        env.replay(0)
+        env.replay(0)
+        torch.cuda.synchronize()
+        assert not env.roll_gave_up()
+        env.close()
 
 
 def test_roll_ragged_episodes_match_chain():
@@ -101,21 +136,19 @@ def test_roll_ragged_episodes_match_chain():
     B, N, T = 8192, 24, 100
     env = _env(scenario="mixed", n_agents=N, n_envs=B, n_agents_min=3, seed=5, episode_length=T)
     acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
-    env.reset(seed=5)
+    _fresh(env, 5)
     env.capture(acts, T, slot=0, kernels="both")
     for _ in range(3):
         env.replay(0)
     torch.cuda.synchronize()
     ref = {k: v.clone() for k, v in env.t.items()}
-    env.reset(seed=5)
-    env.t["lsa_stats"].zero_()
+    _fresh(env, 5)
     env.capture(acts, T, slot=1, kernels="roll")
     assert env.graph_is_rollout(1)
     for _ in range(3):
         env.replay(1)
     torch.cuda.synchronize()
     assert not env.roll_gave_up()
-    ref["lsa_stats"] = env.t["lsa_stats"].clone()
     _same(ref, env, "3 episodes")
     env.close()
 

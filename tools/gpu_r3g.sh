@@ -1,5 +1,5 @@
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r3_f; mkdir -p $O
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r3_g; mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_roll_ragged.py -x -v --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_rr.log 2>&1; rc=$?
 grep -E "PASS|FAIL|ERROR|passed|failed" $O/pytest_rr.log | tail -25
 [ $rc -eq 0 ] || { grep -B2 -A30 "Error\|assert" $O/pytest_rr.log | head -60; exit 2; }
@@ -7,4 +7,3 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_roll.py tests/test_gpu_roll
 tail -1 $O/pytest_roll.log
 timeout -k 10 300 python bench.py --config c4 --no-cpu-baseline > $O/bench_c4.json 2> $O/bench_c4.err || { tail -20 $O/bench_c4.err; exit 4; }
 python -c "import json;d=json.load(open('$O/bench_c4.json'));r=d['roofline'];print('c4', d['value'], d['ms_per_step'], r['kernel'], r['mean_launch_us'], d.get('assignment'))"
-bash tools/gpu_ab.sh r3_f_ab graph lag2
