@@ -349,6 +349,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-align", action="store_true",
                     help="do not advance (untimed) so that the timed region contains an episode boundary")
     ap.add_argument("--eager", action="store_true", help="launch steps eagerly instead of HIP graphs")
+    ap.add_argument("--policy", action="store_true",
+                    help="closed loop: GpuGraphVecEnv(output='torch', graph='coo').step() with an on-device "
+                         "greedy policy reading each step's obs (the runner's path; context, not the headline)")
     ap.add_argument("--unfused", action="store_true",
                     help="two launches per step in the graphs (no lagged emission)")
     ap.add_argument("--no-roll", action="store_true",
@@ -476,7 +479,14 @@ def run_rank(args):
         spec["n_envs"] = args.n_envs
     N, B = spec["n_agents"], spec["n_envs"]
     cfg = shard_config(EnvConfig(seed=1234, **spec), rank, world)
-    env = make_env(cfg, dev)
+    venv = None
+    if args.policy and not stub:
+        # the vec-env a GS-MARL runner drives (gsmarl_amd/vec_env.py), on device
+        from gsmarl_amd.vec_env import GpuGraphVecEnv
+        venv = GpuGraphVecEnv(cfg, dev, output="torch", graph="coo")
+        env = venv.batch
+    else:
+        env = make_env(cfg, dev)
     EL = cfg.episode_length
     gen = torch.Generator(device=dev)
     gen.manual_seed(1000 + rank)
@@ -488,7 +498,8 @@ def run_rank(args):
     chunk = min(K, EL)
     n_chunks, rem = divmod(K, chunk)
     gk = "unfused" if args.unfused else "both"
-    roll = not (args.unfused or args.no_roll or args.eager or stub)
+    eager = args.eager or args.policy
+    roll = not (args.unfused or args.no_roll or eager or stub)
 
     def capture(n, slot):
         """A graph of n steps: the fused rollout where the config has one
@@ -503,7 +514,7 @@ def run_rank(args):
                 roll = False
         env.capture(actions, n, timing=False, slot=slot, kernels=gk)
 
-    if not args.eager:
+    if not eager:
         if W > 0:
             capture(W, 2)
         if A > 0:   # slot 3 is re-captured later by the roofline timing
@@ -512,8 +523,22 @@ def run_rank(args):
         if rem:
             capture(rem, 1)
 
+    obs = env.outputs()["obs"] if venv is not None else None
+
+    def greedy(o):
+        """a trivial policy on device: the discrete action along the larger
+        component of (target - position) (obs[..., 4:6]; actions 1/2 = +x/-x,
+        3/4 = +y/-y)"""
+        dx, dy = o[..., 4], o[..., 5]
+        return torch.where(dx.abs() > dy.abs(), torch.where(dx > 0, 1, 2),
+                           torch.where(dy > 0, 3, 4)).to(torch.int32)
+
     def run_steps(n, slot):
-        if args.eager:
+        nonlocal obs
+        if venv is not None:
+            for t in range(n):
+                obs = venv.step(greedy(obs))[0]
+        elif args.eager:
             for t in range(n):
                 env.step(actions[t % EL], sync_edges=False)
         else:
@@ -595,7 +620,7 @@ def run_rank(args):
     # kernel alone, after the timed region. Event nodes between kernels would
     # add their own packet time to every launch.
     roofline = None
-    if not args.no_kernel_timing and not args.eager and not stub:
+    if not args.no_kernel_timing and not eager and not stub:
         roofline = kernel_roofline(env, cfg, actions, args, N, B, EL, roll)
 
     cpu = None
@@ -618,13 +643,15 @@ def run_rank(args):
                        "agents_per_step": agents,
                        "episode_length": EL, "mean_edges_per_env": round(total_edges / B, 2),
                        "parallelism": f"env-sharded x{world} (no data-path collective)",
-                       "launch": "eager" if args.eager else (f"hip-graphs of {chunk} steps" + (
+                       "launch": ("closed loop: GpuGraphVecEnv(output='torch', graph='coo').step(policy(obs)) "
+                                  "per step, greedy on-device policy" if venv is not None else
+                                  "eager" if args.eager else (f"hip-graphs of {chunk} steps" + (
                            (": all steps of a graph and their edges in one fused rollout launch (state on chip; "
                             + ("each env packs its edges a few steps behind its own step through a slab, "
                                "per-wave CSR prefix granules)" if cfg.ragged else "in-launch CSR look-back)"))
                            if roll else ", lagged emission (one launch per step)" if ((seg_cfg or cfg.ragged)
                                                                                      and not args.unfused)
-                           else ", step + emit launch per step"))},
+                           else ", step + emit launch per step")))},
             "timed_region": {"untimed_steps_before": P, "align_steps": A,
                              "episode_boundaries": boundaries_in(P, K, EL),
                              "rank_ms_per_step_max": round(max(times) / K * 1e3, 5),

@@ -30,6 +30,7 @@ struct gsm_handle {
     int32_t *bsum_alt = nullptr;   // second half of the per-workgroup edge-sum double buffer (lagged emission)
     int32_t *block_order = nullptr;   // ragged mixed: workgroup -> env block, heaviest first
     int32_t *order_host = nullptr;    // pinned staging of block_order's async upload
+    int32_t *place_order = nullptr;   // ragged mixed: the rollout's placement order (inside block_order)
     hipEvent_t order_copied = nullptr;   // recorded after the last upload (staging free again)
     struct Slot {
         hipGraph_t graph = nullptr;
@@ -85,26 +86,35 @@ int align16(int x) { return (x + 15) & ~15; }
 // on the caller's stream `s` (from pinned staging), so kernels enqueued on it
 // before the reseed finish with the old order and every later one sees the new
 // order; the staging buffer is reused only after the previous upload read it.
+//
+// The same upload carries the ragged rollout's placement order (after the nb
+// block entries): the grid's W = 4 * ceil(B / 4) envs by descending cost per
+// step, measured linear in N_env per family (tools/probe_c4_balance.py: a
+// uniform batch's time per step is 0.122 us per 1000 units of its SIMDs'
+// load, units 40 + 29 N for polygon/line, 20 + 7 N for navigation); padding
+// envs (b >= B) last. roll_place (gsm_ragged_kernels.hip) deals them to the
+// SIMDs in strata.
 int update_block_order(gsm_handle *h, hipStream_t s) {
     const gsm::DevParams &p = h->dp;
     if (p.path != gsm::kPathRagged || p.scenario != gsm::kScnMixed) return GSM_OK;
     const int nb = h->sz.n_blocks, per = h->sz.envs_per_block;
-    std::vector<int64_t> key(nb);
-    for (int k = 0; k < nb; ++k) {
-        int64_t c = 0;
-        for (int b = k * per; b < (k + 1) * per && b < p.B; ++b) {
-            const int64_t gid = p.env_base + b;
-            const gsm::Philox4 x = gsm::philox4x32_10(0u, 0u, (uint32_t)gid, gsm::kTagShape, p.seed_lo, p.seed_hi);
-            const int n = p.n_min + (int)(((uint64_t)x.x0 * (uint64_t)(p.N - p.n_min + 1)) >> 32);
-            const int64_t ce = (gid % 3) != gsm::kScnNav ? (int64_t)n * n : n;
-            c = ce > c ? ce : c;
-        }
-        key[k] = c;
+    const int W = (p.B + gsm::kWavesPerBlock - 1) / gsm::kWavesPerBlock * gsm::kWavesPerBlock;
+    std::vector<int64_t> key(nb), cost(W, 0);
+    for (int b = 0; b < p.B; ++b) {
+        const int64_t gid = p.env_base + b;
+        const gsm::Philox4 x = gsm::philox4x32_10(0u, 0u, (uint32_t)gid, gsm::kTagShape, p.seed_lo, p.seed_hi);
+        const int n = p.n_min + (int)(((uint64_t)x.x0 * (uint64_t)(p.N - p.n_min + 1)) >> 32);
+        const bool lsa = (gid % 3) != gsm::kScnNav;
+        cost[b] = lsa ? 40 + 29 * (int64_t)n : 20 + 7 * (int64_t)n;
+        const int64_t ce = lsa ? (int64_t)n * n : n;
+        if (b / per < nb && ce > key[b / per]) key[b / per] = ce;
     }
-    std::vector<int32_t> order(nb);
+    std::vector<int32_t> order(nb + W);
     for (int k = 0; k < nb; ++k) order[k] = k;
-    std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return key[a] > key[b]; });
-    const size_t bytes = (size_t)nb * sizeof(int32_t);
+    std::stable_sort(order.begin(), order.begin() + nb, [&](int32_t a, int32_t b) { return key[a] > key[b]; });
+    for (int k = 0; k < W; ++k) order[nb + k] = k;
+    std::stable_sort(order.begin() + nb, order.end(), [&](int32_t a, int32_t b) { return cost[a] > cost[b]; });
+    const size_t bytes = (size_t)(nb + W) * sizeof(int32_t);
     hipError_t e = hipSuccess;
     if (!h->block_order) {
         e = hipMalloc(&h->block_order, bytes);
@@ -132,6 +142,7 @@ int update_block_order(gsm_handle *h, hipStream_t s) {
     e = hipEventRecord(h->order_copied, s);
     if (e != hipSuccess) return hip_fail(h, e, "hipEventRecord (block order)");
     h->dp.block_order = h->block_order;
+    h->place_order = h->block_order + nb;
     return GSM_OK;
 }
 
@@ -663,7 +674,7 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     // graph is dropped
     if (K > gsm::kRollMaxSteps) {
         if (fallback) return kRollIneligible;
-        return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: n_steps must be <= 4095");
+        return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: n_steps must be <= 4094");
     }
     // ragged: per-wave granules, groups of 64 waves (at most 128 groups: one
     // residency round holds <= 8192 waves), edges packed `depth` steps late
@@ -718,7 +729,9 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     // aggregates [K][nb] and inclusive prefixes [K][nb] (look-back). Zeroed
     // once here — granules are tagged with the launch epoch, so replays never
     // clear them
-    const size_t gran_alloc = 16 + (size_t)K * (ragged ? (size_t)(xW + xNG) : 2 * (size_t)nb) * sizeof(uint64_t);
+    // (ragged: then the placement words, gsm::PlaceArea)
+    const size_t gran_alloc = 16 + (size_t)K * (ragged ? (size_t)(xW + xNG) : 2 * (size_t)nb) * sizeof(uint64_t) +
+                              (ragged ? gsm::PlaceArea::words(xW) * sizeof(uint64_t) : 0);
     e = hipMalloc(&sl.gran, gran_alloc);
     if (e != hipSuccess) {
         sl.gran = nullptr;
@@ -762,9 +775,15 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     }
     p.actions = actions;
     p.ro = ro;
+    // ragged mixed: envs dealt to the SIMDs by cost when the grid fills every
+    // SIMD with the same number of waves (GSM_ROLL_PLACE=0: env = wave index)
+    const int place_S = 4 * n_cu;
+    int place_R = 0;
+    if (ragged && h->place_order && xW % place_S == 0) place_R = xW / place_S;
+    if (const char *ev = getenv("GSM_ROLL_PLACE")) if (atoi(ev) == 0) place_R = 0;
     p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, xW, xNG, depth,
-                                  h->sz.max_edges_per_env, 0, sl.gran + 2, h->roll_status, (uint32_t *)sl.gran,
-                                  (int32_t *)h->slab};
+                                  h->sz.max_edges_per_env, place_R, sl.gran + 2, h->roll_status, (uint32_t *)sl.gran,
+                                  (int32_t *)h->slab, place_R ? h->place_order : nullptr, place_S, 0};
     if (e == hipSuccess) {
         what = "rollout kernel node";
         hipKernelNodeParams kp = {};
@@ -821,9 +840,28 @@ int gsm_graph_roll_status(gsm_handle *h, int32_t *gave_up) {
     if (!h->roll_status) return GSM_OK;
     uint32_t v = 0;
     hipError_t e = hipMemcpy(&v, h->roll_status, sizeof v, hipMemcpyDeviceToHost);
-    if (e == hipSuccess && v) e = clear_status(h);
+    if (e == hipSuccess && v) {   // word 0 only (words 1-2: the placement counts)
+        e = gsm::launch_granule_init(h->roll_status, sizeof(uint32_t), 0u, nullptr);
+        if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    }
     if (e != hipSuccess) return hip_fail(h, e, "rollout status read");
     *gave_up = v ? 1 : 0;
+    return GSM_OK;
+}
+
+int gsm_graph_roll_placement(gsm_handle *h, int64_t *dealt, int64_t *fallback) {
+    if (!h || !dealt || !fallback) return fail(h, GSM_EINVAL, "NULL argument");
+    *dealt = *fallback = 0;
+    if (!h->roll_status) return GSM_OK;
+    uint32_t v[2] = {0, 0};
+    hipError_t e = hipMemcpy(v, h->roll_status + 1, sizeof v, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && (v[0] || v[1])) {
+        e = gsm::launch_granule_init(h->roll_status + 1, sizeof v, 0u, nullptr);
+        if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    }
+    if (e != hipSuccess) return hip_fail(h, e, "rollout placement read");
+    *fallback = v[0];
+    *dealt = v[1];
     return GSM_OK;
 }
 

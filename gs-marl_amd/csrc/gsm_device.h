@@ -130,9 +130,29 @@ __device__ __forceinline__ int wave_scan(int v) {
         __builtin_amdgcn_sched_barrier(0);                                                        \
         if ((p).stamps && (threadIdx.x & 63) == 0) (p).stamps[(int64_t)(wave_id)*16 + (k)] = t_;  \
     } while (0)
+// cycles since t0 (a GSM_TNOW) added to p.stamps[wave][k] (vector atomic)
+#define GSM_TNOW(var)                                                                             \
+    unsigned long long var;                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                                            \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(var)::"memory");                  \
+    __builtin_amdgcn_sched_barrier(0)
+#define GSM_ACC(p, wave_id, k, t0)                                                                \
+    do {                                                                                          \
+        GSM_TNOW(t1_);                                                                            \
+        if ((p).stamps && (threadIdx.x & 63) == 0)                                                \
+            __hip_atomic_fetch_add((p).stamps + (int64_t)(wave_id)*16 + (k), t1_ - (t0),          \
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);                   \
+    } while (0)
+#define GSM_SET(p, wave_id, k, val)                                                               \
+    do {                                                                                          \
+        if ((p).stamps && (threadIdx.x & 63) == 0) (p).stamps[(int64_t)(wave_id)*16 + (k)] = (val); \
+    } while (0)
 #else
 #define GSM_STAMP(p, wave_id, k) do { (void)(wave_id); } while (0)
 #define GSM_RSTAMP(p, wave_id, k) do { (void)(wave_id); } while (0)
+#define GSM_TNOW(var) do { } while (0)
+#define GSM_ACC(p, wave_id, k, t0) do { (void)(wave_id); } while (0)
+#define GSM_SET(p, wave_id, k, val) do { (void)(wave_id); } while (0)
 #endif
 
 // number of set bits of `mask` below this lane

@@ -26,7 +26,8 @@ __host__ __device__ constexpr int lsa_lds_bytes(int nmax) {
 constexpr int kMaxSegEnvsPerWave = 4;
 // steps of one rollout launch (the step field of the 32-bit granule tags,
 // gsm_device.h roll_epoch_tag)
-constexpr int kRollMaxSteps = 4095;
+// (step field 4095 tags the ragged rollout's placement words, PlaceArea)
+constexpr int kRollMaxSteps = 4094;
 
 // Everything a launch needs, passed by value (kernarg segment, < 4 KB).
 // fp32 constants are formed on the host exactly as oracle/batch_ref.py:Spec
@@ -106,11 +107,14 @@ struct DevParams {
         int32_t n_actions, t_first, K;
         int32_t xW, xNG;      // per-wave hand-off (ragged rollout): waves of the grid, groups of 64 (gsm_device.h Xfer)
         int32_t depth;        // ragged rollout: steps between an env's step and the packing of its edges
-        int32_t slab_e, pad;  // ragged rollout: edges per env slab (the config's max_edges_per_env)
+        int32_t slab_e;       // ragged rollout: edges per env slab (the config's max_edges_per_env)
+        int32_t place_R;      // ragged rollout placement: waves per SIMD when the grid fills every SIMD
         uint64_t *gran;
         uint32_t *status;
         uint32_t *epoch;
         int32_t *slab;        // ragged rollout: [depth + 1][B] slabs of [2][slab_e] int32 + [slab_e] f32
+        const int32_t *place; // ragged rollout: [W] envs by descending cost (nullptr: env = wave index)
+        int32_t place_S, pad; // SIMDs the grid fills (place_R * place_S = W)
     } roll;
     // A rollout's per-step outputs: step k's at base + k * stride (elements;
     // stride 0 = every step into the bound buffers, > 0 = a rollout buffer's
@@ -179,6 +183,21 @@ const void *step_ragged_kernel_fn();
 const void *roll_ragged_kernel_fn(const DevParams &p, bool slots);
 size_t roll_ragged_kernel_lds(const DevParams &p);
 constexpr int kRaggedRollMaxDepth = 8;
+// The ragged rollout's SIMD-balanced placement (gsm_ragged_kernels.hip
+// roll_place): u64 words after its per-wave granules. SIMD keys are 13 bits
+// of HW_ID / XCC_ID.
+struct PlaceArea {
+    static constexpr int kKeys = 8192;
+    static constexpr int kMask = 0;                 // [kKeys] {tag, wave-slot bits}
+    static constexpr int kRank = kKeys;             // [kKeys] {tag, SIMD index within its XCC}
+    static constexpr int kBad = 2 * kKeys;          // {tag, 0}: a SIMD holds more than place_R waves
+    static constexpr int kGroups = 64;              // counter groups: XCC x shader engine
+    static constexpr int kArrive = 2 * kKeys + 8;   // [kGroups] workgroups arrived, one per 64 bytes
+    static constexpr int kNsimd = kArrive + 8 * kGroups;   // [kGroups] SIMDs seen, one per 64 bytes
+    static constexpr int kMode = kNsimd + 8 * kGroups;     // [kGroups] {tag, decision} replicas, one per 64 bytes
+    static constexpr int kClaim = kMode + 8 * kGroups;     // [W] u32 tags: the env claimed this launch
+    static constexpr size_t words(int W) { return (size_t)kClaim + ((size_t)W + 1) / 2; }
+};
 const void *lag_step_ragged_kernel_fn();   // kLag: the previous step's emission first
 const void *step_tile_kernel_fn();
 const void *emit_tile_kernel_fn();

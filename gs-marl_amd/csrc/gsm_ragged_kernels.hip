@@ -1067,13 +1067,158 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_ragged_kernel(DevParams p) {
 // per wave after the step kernel's LDS: the stashed lane state, the counts
 // (N_max = 24 mixed: 3616 + 1072 B per wave, 18.8 KB per workgroup: eight
 // workgroups per CU, so 8192 envs take one residency round)
+// ---- SIMD-balanced placement (ragged mixed batches). A launch is as slow
+// as its most loaded SIMD: every env trails the others by at most `depth`
+// steps, and a SIMD's eight waves share its issue. With env e on wave e, a
+// SIMD's load is the sum of eight random envs' costs (N from 3 to 24,
+// navigation or polygon/line: max / mean ~1.7 over 1024 SIMDs). So each wave
+// first learns which SIMD it runs on (HW_ID, XCC_ID), and once every wave has
+// registered the envs are dealt by cost: sorted descending (p.roll.place,
+// host), stratum r (the wave's rank among its SIMD's waves) holds the
+// S = place_S envs r*S .. r*S+S-1, snaked over the SIMDs (SIMD i takes entry
+// i of even strata, S-1-i of odd ones). Each SIMD then holds one env of every
+// cost stratum. Waits on envs handled by any wave are safe only when every
+// wave is resident; that is decided from the registrations: all W arrive
+// within kPlaceWaitTicks and exactly place_S SIMDs hold them with no SIMD
+// above place_R -> dealt; else (another kernel holds CUs: partial
+// residency) env = wave index, whose waits are on earlier-dispatched waves
+// only. Registration uses returning atomics only (each completes before the
+// next is issued) on words tagged with this launch's epoch, so nothing needs
+// clearing except the arrival / SIMD counters, which the epoch bumper zeroes
+// at the end of the launch; a wrong decision cannot go unnoticed (every env
+// is claimed by a tagged exchange: a second claim sets status 4, a missing
+// env times its successors out).
+constexpr uint64_t kPlaceWaitTicks = 40000;   // 400 us of s_memrealtime
+constexpr uint32_t kPlaceIdentity = 1, kPlaceDealt = 2;
+__device__ __forceinline__ uint64_t place_ld(const uint64_t *g) {   // a wave-uniform atomic load
+    const uint64_t x = __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32 |
+           __builtin_amdgcn_readfirstlane((uint32_t)x);
+}
+__device__ __forceinline__ uint64_t *place_area(const KernargParams &q) {
+    return q.roll.gran + 2 + (int64_t)q.roll.K * (q.roll.xW + q.roll.xNG);
+}
+// Registration counters are spread over kGroups words (XCC x shader engine)
+// so that no word takes more than ~128 atomics per launch.
+__device__ int roll_place(const int wg_wave, const uint32_t epoch) {
+    KernargParams &q = late_params();
+    if (q.roll.place == nullptr) return wg_wave;
+    const int lane = threadIdx.x & 63;
+    const uint32_t ptag = roll_epoch_tag(epoch) | 0xfffu;
+    uint64_t *const A = place_area(q);
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);          // HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;   // XCC_ID
+    const uint32_t grp = (xcc << 3) | ((hw >> 13) & 7u);                    // XCC, shader engine
+    const int key = (int)((grp << 7) | (((hw >> 12) & 1u) << 6) | (((hw >> 8) & 15u) << 2) | ((hw >> 4) & 3u));
+    const uint32_t slot = hw & 15u;
+    const int R = q.roll.place_R, S = q.roll.place_S;
+    if (lane == 0) {   // returning atomics only: each completes before the next is issued
+        gu64 *mk = (gu64 *)(A + PlaceArea::kMask + key);
+        uint64_t x = __hip_atomic_load(mk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), have;
+        for (;;) {
+            have = (uint32_t)(x >> 32) == ptag ? x : (uint64_t)ptag << 32;
+            if (__hip_atomic_compare_exchange_strong(mk, &x, have | (1ull << slot), __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+                break;
+        }
+        const int before = __popc((uint32_t)have);
+        if (before == 0) {   // the SIMD's first wave: its index within the group
+            const uint64_t il = __hip_atomic_fetch_add((gu64 *)(A + PlaceArea::kNsimd + 8 * grp), 1ull,
+                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            (void)__hip_atomic_exchange((gu64 *)(A + PlaceArea::kRank + key), (uint64_t)ptag << 32 | (uint32_t)il,
+                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (before + 1 > R)
+            (void)__hip_atomic_exchange((gu64 *)(A + PlaceArea::kBad), (uint64_t)ptag << 32, __ATOMIC_RELAXED,
+                                        __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();   // the workgroup's waves have registered: one arrival for all four
+    if (threadIdx.x == 0)
+        (void)__hip_atomic_fetch_add((gu64 *)(A + PlaceArea::kArrive + 8 * grp), 1ull, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+    // The decision, by workgroup 0's first wave (dispatched first, so always
+    // resident): it polls the arrival counters and publishes to one replica
+    // of the decision per counter group; every other wave polls its group's
+    // replica only (8192 waves polling the counters themselves kept the
+    // registrations waiting ~300 us).
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint32_t dec = 0;
+    if (wg_wave == 0) {
+        for (;;) {
+            const uint64_t a = __hip_atomic_load((gu64 *)(A + PlaceArea::kArrive + 8 * lane), __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+            const int arrived = wave_total((int)a);
+            const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t0;
+            if (arrived == (int)gridDim.x) {
+                const uint64_t n = __hip_atomic_load((gu64 *)(A + PlaceArea::kNsimd + 8 * lane), __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t bad = place_ld(A + PlaceArea::kBad);
+                dec = (wave_total((int)n) == S && (uint32_t)(bad >> 32) != ptag) ? kPlaceDealt : kPlaceIdentity;
+                break;
+            }
+            if (dt > kPlaceWaitTicks) {
+                dec = kPlaceIdentity;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        (void)__hip_atomic_exchange((gu64 *)(A + PlaceArea::kMode + 8 * lane), (uint64_t)ptag << 32 | dec,
+                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+        for (;;) {
+            const uint64_t m = place_ld(A + PlaceArea::kMode + 8 * grp);
+            if ((uint32_t)(m >> 32) == ptag) {
+                dec = (uint32_t)m;
+                break;
+            }
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kRollSpinTicks) {
+                if (lane == 0)
+                    __hip_atomic_store((gu32 *)q.roll.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                dec = kPlaceIdentity;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(8);
+        }
+    }
+    dec = __builtin_amdgcn_readfirstlane(dec);
+    GSM_SET(q, wg_wave, 12, (uint64_t)dec);   // diagnostic builds: the decision and its wait
+    GSM_SET(q, wg_wave, 13, __builtin_amdgcn_s_memrealtime() - t0);
+    if (dec != kPlaceDealt) return wg_wave;
+    // stratum r: the wave's rank among its SIMD's waves; i: the SIMD's index
+    // (SIMDs of lower groups first)
+    const uint64_t mk = place_ld(A + PlaceArea::kMask + key);
+    uint64_t rk = place_ld(A + PlaceArea::kRank + key);
+    while ((uint32_t)(rk >> 32) != ptag) {   // published before its wave arrived: normally at once
+        __builtin_amdgcn_s_sleep(1);
+        rk = place_ld(A + PlaceArea::kRank + key);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kRollSpinTicks) {
+            if (lane == 0) __hip_atomic_store((gu32 *)q.roll.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return wg_wave;
+        }
+    }
+    const uint64_t nx = lane < (int)grp ? __hip_atomic_load((gu64 *)(A + PlaceArea::kNsimd + 8 * lane),
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    const int i = (int)(uint32_t)rk + wave_total((int)nx);
+    const int r = __popc((uint32_t)mk & ((1u << slot) - 1u));
+    const int pos = r * S + ((r & 1) ? S - 1 - i : i);
+    const int env = __builtin_amdgcn_readfirstlane(q.roll.place[pos]);
+    if (lane == 0) {
+        const uint32_t old = __hip_atomic_exchange((gu32 *)((uint32_t *)(A + PlaceArea::kClaim) + env), ptag,
+                                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (old == ptag) __hip_atomic_store((gu32 *)q.roll.status, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return env;
+}
+
 constexpr int kRaggedRollWaveLds = 16 * kRaggedMaxAgents + 8 * kWave + ((4 * (kRaggedRollMaxDepth + 1) + 15) & ~15);
 template <bool kSlots>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void gsm_roll_ragged_kernel(
     DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int w = (int)blockIdx.x * kWavesPerBlock + wave;   // the env
+    const uint32_t epoch = *p.roll.epoch;
+    // the env this wave runs (SIMD-balanced placement, or the wave's index)
+    const int w = __builtin_amdgcn_readfirstlane(roll_place((int)blockIdx.x * kWavesPerBlock + wave, epoch));
     const int Nmax = p.N, Tmax = p.T, Emax = p.E;
     const bool live = w < p.B;
     const int64_t eb = live ? w : 0;
@@ -1085,6 +1230,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     int *s_cnt = (int *)(s_rm + kWave);                          // [depth + 1] the env's edge counts by step
     const int D = p.roll.depth, K = p.roll.K, n_act = p.roll.n_actions;
     int lane = threadIdx.x & 63;
+    GSM_RSTAMP(p, w, 0);
+#ifdef GSM_STAMPS   // diagnostic builds: where the wave runs
+    GSM_SET(p, w, 8, (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4));    // HW_ID
+    GSM_SET(p, w, 9, (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20));   // XCC_ID
+#endif
 
     // ---- the state before step t_first
     int t = 0, ep = 0;
@@ -1101,7 +1251,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         if (lane < s.T) tp = pos_b[Nmax + lane];
         if (lane < s.N) v = p.vel[eb * Nmax + lane];
     }
-    const uint32_t epoch = *p.roll.epoch;
     auto xf = [&]() -> Xfer {
         KernargParams &q = late_params();
         Xfer x;
@@ -1193,6 +1342,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     for (int k = 0; k < K; ++k) {
         lane = threadIdx.x & 63;
         asm volatile("" : "+v"(lane));
+        GSM_TNOW(tk0);
         // (the hand-off's granules are loaded where they are used: published
         // steps earlier, they normally land without a wait, and held across
         // the assignment they would cost the 64-VGPR budget scratch spills)
@@ -1239,7 +1389,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         t += 1;
         const bool done = live && t >= P().EL;
         // a group's last wave: the group sum of step k - 1
+        GSM_ACC(late_params(), w, 3, tk0);
+        GSM_TNOW(tk1);
         if (k >= 1 && glast) xfer_grp_publish(xf(), xfer_grp_load(xf(), k - 1, w, lane), k - 1, w, lane, cur_edges);
+        GSM_ACC(late_params(), w, 5, tk1);
+        GSM_TNOW(tk2);
 
         int cnt = 0;
         rmask = pair_sweep(&cnt);
@@ -1276,7 +1430,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
                 r = -sqrtf(dx * dx + dy * dy);
             }
         } else {
+            GSM_ACC(late_params(), w, 4, tk2);   // sweep + publish
+            GSM_TNOW(tk3);
             r = -assign();
+            GSM_ACC(late_params(), w, 6, tk3);   // assignment
         }
         float rsum = wave_sum(lane < s.N ? r : 0.0f);
         if (P().shared_reward) {
@@ -1368,10 +1525,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         }
         if (k == K - 1 && q.degenerate && lane == 0) {}   // flags written with the final state
         // the edges of step k - depth
+        GSM_TNOW(tk4);
         if (k >= D) pack(k - D, xfer_off_settle(xf(), xfer_off_load(xf(), k - D, w, lane), k - D, w, lane));
+        GSM_ACC(late_params(), w, 7, tk4);
         arow = arow + 1 == n_act ? 0 : arow + 1;
         ring = ring == D ? 0 : ring + 1;
     }
+    GSM_RSTAMP(late_params(), w, 1);
     // ---- the tail: the last group sums, the last `depth` steps' edges, the
     // last step's edge sums per env block (later eager emit launches)
     for (int k = K; k < K + D; ++k) {
@@ -1401,6 +1561,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         __hip_atomic_store((gu32 *)q.roll.epoch, roll_next_epoch(epoch), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     }
+    // every wave has registered and decided: the placement counters for the
+    // next launch (one per lane), and this launch's decision counted
+    if (w == xf().W - 1 && late_params().roll.place) {
+        KernargParams &q = late_params();
+        uint64_t *const A = place_area(q);
+        __hip_atomic_store((gu64 *)(A + PlaceArea::kArrive + 8 * lane), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store((gu64 *)(A + PlaceArea::kNsimd + 8 * lane), 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t m = place_ld(A + PlaceArea::kMode);   // (replica 0)
+        const bool dealt = (uint32_t)(m >> 32) == (roll_epoch_tag(epoch) | 0xfffu) && (uint32_t)m == kPlaceDealt;
+        if (lane == 0)
+            __hip_atomic_fetch_add((gu32 *)(q.roll.status + (dealt ? 2 : 1)), 1u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+    GSM_RSTAMP(late_params(), w, 2);
     // ---- the final state (what the next launch or an eager step reads)
     if (!live) return;
     KernargParams &q = late_params();

@@ -331,6 +331,15 @@ class GpuBatchEnv:
         self._chk(self.lib.gsm_graph_roll_status(self._h, C.byref(v)), "gsm_graph_roll_status")
         return bool(v.value)
 
+    def roll_placement(self) -> tuple:
+        """(dealt, fell_back): ragged mixed rollout launches since the last
+        call that dealt their envs to the SIMDs by cost, and that ran env =
+        wave index because not every wave was resident (gsm.h
+        gsm_graph_roll_placement); clears the counts. Synchronises."""
+        d, f = C.c_int64(), C.c_int64()
+        self._chk(self.lib.gsm_graph_roll_placement(self._h, C.byref(d), C.byref(f)), "gsm_graph_roll_placement")
+        return int(d.value), int(f.value)
+
     def graph_kernel_ms(self, slot: int = 0):
         """(mean step-kernel ms, mean emit-kernel ms, whole-graph ms) of the
         last replay of a timed graph."""

@@ -37,8 +37,9 @@ extern "C" {
  *    gsm_buffers.degenerate */
 /* 6: fused rollout graphs (GSM_GRAPH_ROLL, gsm_graph_roll_status, gsm_graph_info)
  * 7: gsm_get_state / gsm_set_state; rollout graphs emit every step's edges in
- *    their one launch (no separate emit launch) */
-#define GSM_ABI_VERSION 7
+ *    their one launch (no separate emit launch)
+ * 8: ragged rollouts (n_steps <= 4094), gsm_graph_roll_placement */
+#define GSM_ABI_VERSION 8
 
 typedef enum gsm_status {
     GSM_OK = 0,
@@ -267,7 +268,7 @@ int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream);
 #define GSM_GRAPH_TIME_ENDS 8
 #define GSM_GRAPH_UNFUSED 16
 #define GSM_GRAPH_LAG_ONLY 32
-/* GSM_GRAPH_ROLL: all n_steps (<= 4095) steps and their edges run in ONE
+/* GSM_GRAPH_ROLL: all n_steps (<= 4094) steps and their edges run in ONE
  * launch (navigation configs with a compiled rollout shape — 3, 6, 12 or 24
  * agents with as many obstacles, one env per wave — the tile path, one env
  * per workgroup, and ragged batches, one env per wave; the whole batch in one
@@ -301,6 +302,11 @@ int gsm_graph_info(gsm_handle *h, int32_t slot, int32_t *steps, int32_t *fused);
  * wait) timed out since the last call (that launch's edges are then invalid),
  * else 0. Clears the flag. Synchronises (reads a device word). */
 int gsm_graph_roll_status(gsm_handle *h, int32_t *gave_up);
+/* Ragged mixed rollouts deal their envs to the SIMDs by estimated cost when
+ * every wave of the launch is resident (else env = wave index; same outputs
+ * either way). After launches have completed: how many dealt their envs and
+ * how many fell back since the last call. Clears the counts; synchronises. */
+int gsm_graph_roll_placement(gsm_handle *h, int64_t *dealt, int64_t *fallback);
 /* After a timed launch of `slot` has completed: mean duration (ms) of the
  * step and emit kernels (TIME_EACH), and the whole graph (both flags). */
 int gsm_graph_kernel_ms(gsm_handle *h, int32_t slot, float *step_mean_ms, float *emit_mean_ms,

@@ -1,0 +1,80 @@
+"""Rollouts while another kernel holds CUs (a stand-in for the RCCL
+all-reduce that C5 overlaps with the chunk's rollout).
+
+Spin kernels on side streams take wave slots first, so the rollout grid no
+longer fits in one residency round. The headline (segmented) rollout must
+still progress — a workgroup waits only on lower-numbered ones, dispatched
+before it — and the ragged rollout must fall back from its SIMD-balanced
+placement to env = wave index (its waits are then on earlier-dispatched waves
+only). Either way no bounded wait gives up and every buffer equals eager
+steps bit for bit."""
+import time
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _env(**kw):
+    from gsmarl_amd import EnvConfig, GpuBatchEnv
+    return GpuBatchEnv(EnvConfig(**kw), DEV)
+
+
+def _reset(env, seed, ragged):
+    env.reset(seed=seed)
+    if ragged:   # equal runs start from equal assignment warm-start caches
+        env.t["lsa_v"].zero_()
+        env.t["lsa_col"].fill_(-1)
+        env.t["lsa_stats"].zero_()
+
+
+def _hog(n_streams=4, cycles=50_000_000):
+    """one spinning single-wave kernel per side stream"""
+    streams = [torch.cuda.Stream(device=DEV) for _ in range(n_streams)]
+    for s in streams:
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(cycles)
+    return streams
+
+
+@pytest.mark.parametrize("kind", ["h", "c4"])
+def test_roll_with_cus_taken(kind):
+    ragged = kind == "c4"
+    kw = dict(n_agents=24, n_envs=8192, seed=3, episode_length=100)
+    if ragged:
+        kw.update(scenario="mixed", n_agents_min=3)
+    env = _env(**kw)
+    T = 20
+    acts = torch.randint(0, 5, (T, 8192, 24), dtype=torch.int32, device=DEV)
+    _reset(env, 3, ragged)
+    for t in range(T):
+        env.step(acts[t], sync_edges=False)
+    torch.cuda.synchronize()
+    ref = {k: v.clone() for k, v in env.t.items()}
+    _reset(env, 3, ragged)
+    env.capture(acts, T, slot=0, kernels="roll")
+    assert env.graph_is_rollout(0)
+    if ragged:
+        env.roll_placement()   # clear the counts
+    torch.cuda.synchronize()
+    streams = _hog()
+    time.sleep(0.005)          # the spin kernels are resident first
+    env.replay(0)
+    torch.cuda.synchronize()
+    for s in streams:
+        s.synchronize()
+    assert not env.roll_gave_up()
+    n = int(ref["edge_ptr"][-1])
+    for k in ref:
+        if k in ("edge_index", "edge_attr"):   # the valid edges (eager steps leave earlier steps' past n)
+            assert torch.equal(ref[k][..., :n], env.t[k][..., :n]), k
+        else:
+            assert torch.equal(ref[k], env.t[k]), k
+    if ragged:
+        dealt, fell_back = env.roll_placement()
+        print(f"placement: dealt {dealt}, fell back {fell_back}")
+        assert dealt + fell_back == 1
+    env.close()

@@ -5,8 +5,9 @@ per-env slab. Every state and output buffer must equal the
 eager steps' bit for bit (which test_gpu_ragged checks against the oracle):
 partial workgroups, auto-resets inside the launch, all three action formats,
 pack depths 2..8, repeated replays, rollout-buffer slots (assignments
-included), three full-size C4 episodes against the lagged chain, and the last
-step of a launch against oracle/ragged_ref.py directly."""
+included), three full-size C4 episodes against the lagged chain (envs dealt
+to the SIMDs by cost), and the last step of a launch against
+oracle/ragged_ref.py directly."""
 import os
 
 import numpy as np
@@ -70,6 +71,7 @@ def depth(request):
     (None, "mixed", 24, 257, 9, 3, "index"), (None, "mixed", 24, 64, 2, 5, "index"),
     (None, "mixed", 24, 40, 1, 5, "index"), (None, "polygon", 12, 130, 7, 4, "onehot"),
     (None, "line", 9, 64, 5, 3, "cont"), (None, "mixed", 24, 8192, 12, 5, "index"),
+    (None, "mixed", 24, 4096, 6, 4, "onehot"),
     (2, "mixed", 24, 300, 11, 4, "index"), (8, "mixed", 24, 300, 11, 4, "index"), (8, "polygon", 24, 100, 3, 2, "index"),
 ], indirect=["depth"])
 def test_roll_ragged_equals_eager(depth, scenario, N, B, T, EL, fmt):
@@ -145,11 +147,14 @@ def test_roll_ragged_episodes_match_chain():
     _fresh(env, 5)
     env.capture(acts, T, slot=1, kernels="roll")
     assert env.graph_is_rollout(1)
+    env.roll_placement()
     for _ in range(3):
         env.replay(1)
     torch.cuda.synchronize()
     assert not env.roll_gave_up()
     _same(ref, env, "3 episodes")
+    # on an idle GPU every launch deals its envs to the SIMDs by cost
+    assert env.roll_placement() == (3, 0)
     env.close()
 
 
