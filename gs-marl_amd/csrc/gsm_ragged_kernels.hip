@@ -1064,9 +1064,6 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_ragged_kernel(DevParams p) {
 // steps. In the bound buffers the earlier steps' edges go to the library
 // scratch (roll_edge_sink): only the last step's may land in the shared
 // outputs.
-// per wave after the step kernel's LDS: the stashed lane state, the counts
-// (N_max = 24 mixed: 3616 + 1072 B per wave, 18.8 KB per workgroup: eight
-// workgroups per CU, so 8192 envs take one residency round)
 // ---- SIMD-balanced placement (ragged mixed batches). A launch is as slow
 // as its most loaded SIMD: every env trails the others by at most `depth`
 // steps, and a SIMD's eight waves share its issue. With env e on wave e, a
@@ -1210,7 +1207,12 @@ __device__ int roll_place(const int wg_wave, const uint32_t epoch) {
     return env;
 }
 
-constexpr int kRaggedRollWaveLds = 16 * kRaggedMaxAgents + 8 * kWave + ((4 * (kRaggedRollMaxDepth + 1) + 15) & ~15);
+// per wave after the step kernel's LDS: the lane state stashed across the
+// assignment, the next step's forces, the row masks, the counts (N_max = 24
+// mixed: 3616 + 1328 B per wave, 19.8 KB per workgroup: eight workgroups per
+// CU, so 8192 envs take one residency round)
+constexpr int kRaggedRollWaveLds = 16 * kRaggedMaxAgents + 8 * kRaggedMaxAgents + 8 * kWave +
+                                   ((4 * (kRaggedRollMaxDepth + 1) + 15) & ~15);
 template <bool kSlots>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void gsm_roll_ragged_kernel(
     DevParams p) {
@@ -1226,7 +1228,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     const LsaLds s_lsa = lsa_lds(lds, Nmax);                    // assignment scratch
     float2 *s_pos = (float2 *)(lds + lsa_lds_bytes(Nmax));      // [E] staged rows
     float4 *s_stash = (float4 *)(lds + p.wave_lds_step);        // [32] lane state across the assignment
-    uint64_t *s_rm = (uint64_t *)(s_stash + kRaggedMaxAgents);   // [64]
+    float2 *s_fn = (float2 *)(s_stash + kRaggedMaxAgents);       // [32] the next step's forces
+    uint64_t *s_rm = (uint64_t *)(s_fn + kRaggedMaxAgents);      // [64]
     int *s_cnt = (int *)(s_rm + kWave);                          // [depth + 1] the env's edge counts by step
     const int D = p.roll.depth, K = p.roll.K, n_act = p.roll.n_actions;
     int lane = threadIdx.x & 63;
@@ -1280,20 +1283,48 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     uint64_t rmask = 0;             // row masks of the current step (collider lanes)
     bool coinc = false, relaid_any = false;
 
-    // radius row masks and collision counts (as ragged_env_step)
-    auto pair_sweep = [&](int *cnt) {
+    // The forces of a step act at the positions the previous step's sweep
+    // reads, so one pass over the collider pairs serves both: the sweep of
+    // step k also forms the forces of step k + 1. Fn: the agent's force for
+    // the next integration — _set_action's force first, then the contacts in
+    // collider order, the NaN of App. A S16 strict mode last (the operations
+    // and order of ragged_env_step's physics: bit-identical). It waits in LDS
+    // (s_fn) until that integration: held in registers across the step it
+    // would spill.
+    // radius row masks and collision counts (as ragged_env_step) and, with
+    // `nxt`, the forces of the step whose actions are in row `row`
+    auto pair_sweep = [&](int *cnt, const bool nxt, const int row) {
         uint64_t rm = 0;
         int n = 0;
         bool z = false;
+        float Fx = 0.0f, Fy = 0.0f;
+        if (nxt && lane < s.N) {
+            const float2 u = roll_action_force(late_params(), row, eb * Nmax + lane);
+            Fx = u.x;
+            Fy = u.y;
+        }
         for (int c = 0; c < s.M; ++c) {
             const float2 q = rl_f2(cp, c);
             const float dx = cp.x - q.x, dy = cp.y - q.y;
             const float d2 = dx * dx + dy * dy;
-            const bool other = c != lane;
-            n += (other && d2 < (c < s.N ? P().dmin2_aa : P().dmin2_ao)) ? 1 : 0;
+            const bool other = c != lane, ag = c < s.N;
+            n += (other && d2 < (ag ? P().dmin2_aa : P().dmin2_ao)) ? 1 : 0;
             rm |= (other && d2 > 0.0f && d2 <= P().R2) ? (1ull << c) : 0ull;
-            z |= other && d2 == 0.0f && c < s.N;
+            z |= other && d2 == 0.0f && ag;
+            if (nxt && lane < s.N && other && d2 > 0.0f && d2 < (ag ? P().cut2_aa : P().cut2_ao)) {
+                const float f = contact_scale(P(), d2, ag ? P().dmin_aa : P().dmin_ao);
+                Fx += f * dx;
+                Fy += f * dy;
+            }
         }
+        if (nxt && P().strict) {
+            const bool bad = strict_bad(lane, cp, s.N, s.M, [&](int c) { return rl_f2(cp, c); });
+            if (lane < s.N && bad) {
+                Fx = __builtin_nanf("");
+                Fy = __builtin_nanf("");
+            }
+        }
+        if (nxt && lane < kRaggedMaxAgents) s_fn[lane] = make_float2(Fx, Fy);
         *cnt = n;
         coinc = __any(lane < s.M && z);
         return lane < s.M ? rm : 0ull;
@@ -1339,6 +1370,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         }
     };
 
+    {   // the forces of step t_first (its actions, the contacts at the loaded positions)
+        int unused;
+        (void)pair_sweep(&unused, true, arow);
+    }
     for (int k = 0; k < K; ++k) {
         lane = threadIdx.x & 63;
         asm volatile("" : "+v"(lane));
@@ -1346,31 +1381,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         // (the hand-off's granules are loaded where they are used: published
         // steps earlier, they normally land without a wait, and held across
         // the assignment they would cost the 64-VGPR budget scratch spills)
-        // _set_action + apply_environment_force + integrate_state (App. A S3-S6)
-        float Fx = 0.0f, Fy = 0.0f;
-        if (lane < s.N) {
-            const float2 u = roll_action_force(late_params(), arow, eb * Nmax + lane);
-            Fx = u.x;
-            Fy = u.y;
-        }
-        for (int c = 0; c < s.M; ++c) {
-            const float2 q = rl_f2(cp, c);
-            const float dx = cp.x - q.x, dy = cp.y - q.y;
-            const float d2 = dx * dx + dy * dy;
-            const bool ag = c < s.N;
-            if (lane < s.N && c != lane && d2 > 0.0f && d2 < (ag ? P().cut2_aa : P().cut2_ao)) {
-                const float f = contact_scale(P(), d2, ag ? P().dmin_aa : P().dmin_ao);
-                Fx += f * dx;
-                Fy += f * dy;
-            }
-        }
-        if (P().strict) {
-            const bool bad = strict_bad(lane, cp, s.N, s.M, [&](int c) { return rl_f2(cp, c); });
-            if (lane < s.N && bad) {
-                Fx = __builtin_nanf("");
-                Fy = __builtin_nanf("");
-            }
-        }
+        // integrate_state (App. A S5-S6) with the forces the previous sweep formed
+        const float2 F = lane < kRaggedMaxAgents ? s_fn[lane] : make_float2(0.0f, 0.0f);
+        const float Fx = F.x, Fy = F.y;
+        const int arow_next = arow + 1 == n_act ? 0 : arow + 1;
         if (lane < s.N) {
             v.x = v.x * P().omd;
             v.y = v.y * P().omd;
@@ -1396,7 +1410,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         GSM_TNOW(tk2);
 
         int cnt = 0;
-        rmask = pair_sweep(&cnt);
+        rmask = pair_sweep(&cnt, k + 1 < K, arow_next);
         if (lane >= s.N) cnt = 0;
         const bool will_reset = done && P().auto_reset;
         if (!will_reset) publish(k);   // ahead of the assignment
@@ -1466,7 +1480,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             if (lane < s.M) cp = layout_at(P(), s, gid, (uint32_t)ep, lane < s.N ? lane : s.N + s.T + (lane - s.N));
             if (lane < s.T) tp = layout_at(P(), s, gid, (uint32_t)ep, s.N + lane);
             relaid = relaid_any = true;
-            rmask = pair_sweep(&cnt);
+            rmask = pair_sweep(&cnt, k + 1 < K, arow_next);
             if (s.scn != kScnNav) (void)assign();
             publish(k);
         }
@@ -1528,7 +1542,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         GSM_TNOW(tk4);
         if (k >= D) pack(k - D, xfer_off_settle(xf(), xfer_off_load(xf(), k - D, w, lane), k - D, w, lane));
         GSM_ACC(late_params(), w, 7, tk4);
-        arow = arow + 1 == n_act ? 0 : arow + 1;
+        arow = arow_next;
         ring = ring == D ? 0 : ring + 1;
     }
     GSM_RSTAMP(late_params(), w, 1);

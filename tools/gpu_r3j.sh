@@ -1,5 +1,5 @@
 set -o pipefail
-cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r3_l; mkdir -p $O
+cd "$GRAFT_REPO_ROOT"; O=gpurun_out/r3_m; mkdir -p $O
 timeout -k 10 300 python -u -m pytest tests/test_gpu_roll_ragged.py tests/test_gpu_roll_concurrency.py -x -v -s --timeout 120 --timeout-method thread -p no:cacheprovider > $O/pytest_rr.log 2>&1; rc=$?
 grep -E "PASS|FAIL|ERROR|passed|failed|placement" $O/pytest_rr.log | tail -25
 [ $rc -eq 0 ] || { grep -B2 -A30 "Error\|assert" $O/pytest_rr.log | head -60; exit 2; }
