@@ -201,6 +201,75 @@ def test_roll_ragged_last_step_oracle(scenario, N, B):
     env.close()
 
 
+def test_c4_full_size_sampled_oracle():
+    """C4 at full size (mixed, N in {3..24} x 8192): every step of a 12-step
+    run (episode length 5: auto-resets inside) checked on a sample of 85 envs
+    (every 97th) against oracle/ragged_ref.py stepped from the identical fp32
+    state before it — positions / velocities within the 1e-6 bar; edges,
+    assignments, costs, node features and done exact — and the rollout launch
+    of the same 12 steps equal to those eager steps bit for bit (its envs dealt
+    to the SIMDs by cost)."""
+    from gsmarl_amd import EnvConfig
+    B, N, T = 8192, 24, 12
+    cfg = EnvConfig(scenario="mixed", n_agents=N, n_envs=B, n_agents_min=3, seed=31, episode_length=5)
+    keys = set(rr.br.DEFAULTS) | set(rr.RAGGED_DEFAULTS)
+    base = {k: v for k, v in cfg.to_dict().items() if k in keys}
+    env = _env(**cfg.to_dict())
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    sel = np.arange(0, B, 97)
+    _fresh(env, 31)
+    torch.cuda.synchronize()
+    for t in range(T):
+        sh = env.t["env_shape"].cpu().numpy()
+        pos, vel = env.t["pos"].cpu().numpy(), env.t["vel"].cpu().numpy()
+        stp, epi = env.t["step_count"].cpu().numpy(), env.t["episode"].cpu().numpy()
+        acc, last = env.t["ep_acc"].cpu().numpy(), env.t["ep_last"].cpu().numpy()
+        a_np = acts[t].cpu().numpy()
+        env.step(acts[t], sync_edges=False)
+        torch.cuda.synchronize()
+        g = {k: env.t[k].cpu().numpy() for k in ("pos", "vel", "step_count", "episode", "reward", "cost", "done",
+                                                 "assign", "node_feat", "edge_ptr", "edge_index", "edge_attr")}
+        for b in sel:
+            rcfg = rr.make_cfg(**dict(base, n_envs=1, env_base=int(b)))
+            st = dict(pos=pos[b:b + 1], vel=vel[b:b + 1], step=stp[b:b + 1].copy(), episode=epi[b:b + 1].copy(),
+                      ep_acc=acc[b:b + 1].astype(np.float64), ep_last=last[b:b + 1].astype(np.float64),
+                      n=sh[b:b + 1] & 0xFF, scn=sh[b:b + 1] >> 8, seed=31)
+            nst, out = rr.step(rcfg, st, a_np[b:b + 1], 1, np.float64)
+            check_state(g["pos"][b:b + 1], nst["pos"], f"pos c4 t{t} env{b}")
+            check_state(g["vel"][b:b + 1], nst["vel"], f"vel c4 t{t} env{b}")
+            assert g["step_count"][b] == nst["step"][0] and g["episode"][b] == nst["episode"][0], (t, b)
+            assert g["done"][b] == out["done"][0], (t, b)
+            # the observation of the GPU's own fp32 positions: exact
+            ob = rr.observe(rcfg, dict(st, pos=g["pos"][b:b + 1], vel=g["vel"][b:b + 1]))
+            assert np.array_equal(g["assign"][b], ob["assign"][0]), (t, b)
+            assert np.array_equal(g["node_feat"][b], ob["node_feat"][0]), (t, b)
+            lo, hi = int(g["edge_ptr"][b]), int(g["edge_ptr"][b + 1])
+            E = env.E
+            assert np.array_equal(g["edge_index"][:, lo:hi] - b * E, ob["edge_index"]), (t, b)
+            assert np.array_equal(g["edge_attr"][lo:hi], ob["edge_attr"]), (t, b)
+            # cost / reward: the fp32 oracle on the GPU's own post-physics
+            # positions (an env that reset in this step shows its new layout)
+            nb, scb = int(st["n"][0]), int(st["scn"][0])
+            if not g["done"][b]:
+                pc = g["pos"][b, rr.store_index(rr.RSpec(rcfg), scb, nb)]
+                r32, c32, _ = rr.reward_cost_env(rcfg, scb, nb, pc, np.float32)
+                assert np.array_equal(g["cost"][b, :nb], c32), (t, b)
+                if scb != rr.SCN_NAV:   # polygon / line: -C[i][sigma_i], exact
+                    assert np.array_equal(g["reward"][b, :nb], r32), (t, b)
+                else:                   # navigation: -|p - g| within fp32 rounding
+                    np.testing.assert_allclose(g["reward"][b, :nb], r32, rtol=0, atol=2e-6)
+    ref = {k: v.clone() for k, v in env.t.items()}
+    _fresh(env, 31)
+    env.capture(acts, T, slot=0, kernels="roll")
+    env.roll_placement()
+    env.replay(0)
+    torch.cuda.synchronize()
+    assert not env.roll_gave_up()
+    _same(ref, env, "rollout vs eager at C4")
+    assert env.roll_placement() == (1, 0)
+    env.close()
+
+
 def test_roll_ragged_into_buffer_slots():
     """capture_into on a mixed batch is one rollout launch writing slot j's
     outputs (assignments included; edges packed into slot j `depth` steps

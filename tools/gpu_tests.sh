@@ -17,3 +17,8 @@ done
 for n in h_driver h c2 c3 c4; do
   python -c "import json;d=json.load(open('$O/bench_$n.json'));r=d['roofline'];print('$n',d['value'],'us/step',round(d['ms_per_step']*1e3,2),r['kernel'][:22],r['mean_launch_us'],'us frac',r['frac'],'pmc',r['pmc']['status'][:20])"
 done
+# the reference's zero-shot navigation sizes (readme.md:75): rollouts at N = 6, 12
+for n in 6 12; do
+  timeout -k 10 300 python bench.py --n-agents $n --no-cpu-baseline > $O/bench_h_n$n.json 2> $O/bench_h_n$n.err || { tail -20 $O/bench_h_n$n.err; exit 5; }
+  python -c "import json;d=json.load(open('$O/bench_h_n$n.json'));r=d['roofline'];print('h n$n',d['value'],'us/step',round(d['ms_per_step']*1e3,2),r['kernel'][:22],r['mean_launch_us'])"
+done
