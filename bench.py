@@ -346,6 +346,9 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-cores", type=int, default=0, help="host processes for the CPU baseline (0: all, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the roofline timing (null)")
+    ap.add_argument("--settle-ms", type=float, default=0.0,
+                    help="before the warmup, whole untimed episodes (EL steps each, so the alignment holds) "
+                         "until this much wall time has passed with the GPU busy: clocks at their loaded level")
     ap.add_argument("--no-align", action="store_true",
                     help="do not advance (untimed) so that the timed region contains an episode boundary")
     ap.add_argument("--eager", action="store_true", help="launch steps eagerly instead of HIP graphs")
@@ -514,10 +517,13 @@ def run_rank(args):
                 roll = False
         env.capture(actions, n, timing=False, slot=slot, kernels=gk)
 
+    settle = args.settle_ms > 0 and not eager and not stub
     if not eager:
         if W > 0:
             capture(W, 2)
-        if A > 0:   # slot 3 is re-captured later by the roofline timing
+        if settle:   # slot 3 holds a whole episode first, then the alignment
+            capture(EL, 3)
+        elif A > 0:   # slot 3 is re-captured later by the roofline timing
             capture(A, 3)
         capture(chunk, 0)
         if rem:
@@ -544,7 +550,18 @@ def run_rank(args):
         else:
             env.replay(slot)
 
-    # warmup, then the untimed alignment so the timed region holds an auto-reset
+    # settling (whole episodes: the alignment below still holds), warmup, then
+    # the untimed alignment so the timed region holds an auto-reset
+    settle_steps = 0
+    if settle:
+        sync()
+        t_s = time.perf_counter()
+        while (time.perf_counter() - t_s) * 1e3 < args.settle_ms:
+            run_steps(EL, 3)
+            settle_steps += EL
+            sync()
+        if A > 0:
+            capture(A, 3)
     if W > 0:
         run_steps(W, 2)
     if A > 0:
@@ -652,7 +669,8 @@ def run_rank(args):
                            if roll else ", lagged emission (one launch per step)" if ((seg_cfg or cfg.ragged)
                                                                                      and not args.unfused)
                            else ", step + emit launch per step")))},
-            "timed_region": {"untimed_steps_before": P, "align_steps": A,
+            "timed_region": {"untimed_steps_before": P + settle_steps, "align_steps": A,
+                             "settle_steps": settle_steps,
                              "episode_boundaries": boundaries_in(P, K, EL),
                              "rank_ms_per_step_max": round(max(times) / K * 1e3, 5),
                              "rank_ms_per_step_min": round(min(times) / K * 1e3, 5)},

@@ -105,6 +105,41 @@ def main():
     e.record()
     torch.cuda.synchronize(dev)
     res["roll100_b2b_us_per_step"] = round(s.elapsed_time(e) * 1e3 / 500, 3)
+    # the 20-step graph across an episode boundary (every env auto-resets at
+    # step 100: the driver's bench line holds one): advance to step 90 first
+    env.capture(acts, 90, slot=1, kernels="roll")
+    wb, eb = [], []
+    for _ in range(max(3, a.R // 3)):
+        env.reset(seed=1234, sync_edges=False)
+        env.replay(1)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        s.record()
+        env.replay(0)
+        e.record()
+        torch.cuda.synchronize(dev)
+        wb.append((time.perf_counter() - t0) * 1e6)
+        eb.append(s.elapsed_time(e) * 1e3)
+    res[f"roll{a.K}_boundary_us"] = med(wb)
+    res[f"roll{a.K}_boundary_events_us"] = med(eb)
+    # the bench's sequence: 5-step and 85-step graphs, then the timed 20-step
+    # graph's FIRST replay (fresh capture each repetition) vs its later ones
+    first, later = [], []
+    for rep in range(4):
+        env.capture(acts, 5, slot=2, kernels="roll")
+        env.capture(acts, 85, slot=3, kernels="roll")
+        env.capture(acts, a.K, slot=0, kernels="roll")
+        for r2 in range(2):
+            env.reset(seed=1234, sync_edges=False)
+            env.replay(2)
+            env.replay(3)
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            env.replay(0)
+            torch.cuda.synchronize(dev)
+            (first if r2 == 0 else later).append((time.perf_counter() - t0) * 1e6)
+    res[f"roll{a.K}_bench_seq_first_us"] = med(first)
+    res[f"roll{a.K}_bench_seq_second_us"] = med(later)
     res["gave_up"] = bool(env.roll_gave_up())
     print(json.dumps(res), flush=True)
     env.close()
