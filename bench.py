@@ -346,9 +346,10 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-cores", type=int, default=0, help="host processes for the CPU baseline (0: all, <= 16)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true", help="skip the roofline timing (null)")
-    ap.add_argument("--settle-ms", type=float, default=0.0,
+    ap.add_argument("--settle-ms", type=float, default=20.0,
                     help="before the warmup, whole untimed episodes (EL steps each, so the alignment holds) "
-                         "until this much wall time has passed with the GPU busy: clocks at their loaded level")
+                         "until this much wall time has passed with the GPU busy: clocks at their loaded level "
+                         "(the driver's 20-step line: 11.5-11.6 us/step without, 10.85 with 20 ms; DESIGN.md §8)")
     ap.add_argument("--no-align", action="store_true",
                     help="do not advance (untimed) so that the timed region contains an episode boundary")
     ap.add_argument("--eager", action="store_true", help="launch steps eagerly instead of HIP graphs")

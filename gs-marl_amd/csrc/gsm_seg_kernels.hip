@@ -812,6 +812,10 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
             const float2 pi = s_pos[m];
             float Fx = u.x, Fy = u.y;
             uint64_t cm = cand_prev;
+            // (both constants read before the loop: a per-lane select of the
+            // two kernarg fields compiles to a vector load and a vmcnt wait
+            // per contact)
+            const float dmin_aa = pc.dmin_aa, dmin_ao = pc.dmin_ao;
             while (cm) {
                 const int c = __builtin_ctzll(cm);
                 cm &= cm - 1;
@@ -819,7 +823,7 @@ __device__ __forceinline__ int seg_env(const DevParams &p, const Shape<kN, kNo> 
                 const float2 pj = s_pos[row_entity(c, N)];
                 const float dx = pi.x - pj.x, dy = pi.y - pj.y;
                 const float d2 = dx * dx + dy * dy;
-                const float f = contact_scale(pc, d2, ag ? pc.dmin_aa : pc.dmin_ao);
+                const float f = contact_scale(pc, d2, ag ? dmin_aa : dmin_ao);
                 Fx += f * dx;
                 Fy += f * dy;
             }
@@ -1249,6 +1253,10 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             const float2 pi = s_pos[m];
             float Fx = u.x, Fy = u.y;
             uint64_t cm = cand_prev;
+            // (both constants read before the loop: a per-lane select of the
+            // two kernarg fields compiles to a vector load and a vmcnt wait
+            // per contact)
+            const float dmin_aa = pc.dmin_aa, dmin_ao = pc.dmin_ao;
             while (cm) {
                 const int c = __builtin_ctzll(cm);
                 cm &= cm - 1;
@@ -1256,7 +1264,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
                 const float2 pj = s_pos[row_entity(c, N)];
                 const float dx = pi.x - pj.x, dy = pi.y - pj.y;
                 const float d2 = dx * dx + dy * dy;
-                const float f = contact_scale(pc, d2, ag ? pc.dmin_aa : pc.dmin_ao);
+                const float f = contact_scale(pc, d2, ag ? dmin_aa : dmin_ao);
                 Fx += f * dx;
                 Fy += f * dy;
             }
