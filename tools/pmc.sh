@@ -12,7 +12,7 @@ timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 # PMC_ROLL=1: one fused rollout graph of 100 steps (no warmup / alignment graphs)
 LAUNCH="--eager --warmup 10"; [ -n "$PMC_GRAPH" ] && LAUNCH="--no-roll --warmup 10"
 [ -n "$PMC_ROLL" ] && LAUNCH="--warmup 0 --no-align"
-BENCH="$GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-kernel-timing $LAUNCH --steps 100 $*"
+BENCH="$GRAFT_REPO_ROOT/bench.py --no-cpu-baseline --no-kernel-timing --settle-ms 0 $LAUNCH --steps 100 $*"
 i=0
 for grp in "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES" \
            "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INST_CYCLES_SALU GRBM_GUI_ACTIVE" \
