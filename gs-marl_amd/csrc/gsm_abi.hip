@@ -89,9 +89,11 @@ int align16(int x) { return (x + 15) & ~15; }
 //
 // The same upload carries the ragged rollout's placement order (after the nb
 // block entries): the grid's W = 4 * ceil(B / 4) envs by descending cost per
-// step, measured linear in N_env per family (tools/probe_c4_balance.py: a
-// uniform batch's time per step is 0.122 us per 1000 units of its SIMDs'
-// load, units 40 + 29 N for polygon/line, 20 + 7 N for navigation); padding
+// step, linear in N_env per family. Uniform polygon / line batches put
+// polygon/line at ~63 + 27 N (tools/probe_c4_balance.py); navigation envs
+// cannot be run alone on this path, and a scan of the C4 launch time over
+// the navigation weights (tools/gpu_place_model.sh) put them at 55 + 18 N
+// (20 + 7 N: 39.4 us per step, 55 + 18 N: 36.9, 70 + 24 N: 38.9); padding
 // envs (b >= B) last. roll_place (gsm_ragged_kernels.hip) deals them to the
 // SIMDs in strata.
 int update_block_order(gsm_handle *h, hipStream_t s) {
@@ -100,12 +102,25 @@ int update_block_order(gsm_handle *h, hipStream_t s) {
     const int nb = h->sz.n_blocks, per = h->sz.envs_per_block;
     const int W = (p.B + gsm::kWavesPerBlock - 1) / gsm::kWavesPerBlock * gsm::kWavesPerBlock;
     std::vector<int64_t> key(nb), cost(W, 0);
+    // cost units per env and step: polygon/line a + b N, navigation c + d N,
+    // the C4 rollout's best of a scan (tools/gpu_place_model.sh,
+    // GSM_PLACE_MODEL="a,b,c,d" overrides)
+    int64_t ma = 63, mb = 27, mc = 55, md = 18;
+    if (const char *ev = getenv("GSM_PLACE_MODEL")) {
+        long long x[4];
+        if (sscanf(ev, "%lld,%lld,%lld,%lld", &x[0], &x[1], &x[2], &x[3]) == 4) {
+            ma = x[0];
+            mb = x[1];
+            mc = x[2];
+            md = x[3];
+        }
+    }
     for (int b = 0; b < p.B; ++b) {
         const int64_t gid = p.env_base + b;
         const gsm::Philox4 x = gsm::philox4x32_10(0u, 0u, (uint32_t)gid, gsm::kTagShape, p.seed_lo, p.seed_hi);
         const int n = p.n_min + (int)(((uint64_t)x.x0 * (uint64_t)(p.N - p.n_min + 1)) >> 32);
         const bool lsa = (gid % 3) != gsm::kScnNav;
-        cost[b] = lsa ? 40 + 29 * (int64_t)n : 20 + 7 * (int64_t)n;
+        cost[b] = lsa ? ma + mb * (int64_t)n : mc + md * (int64_t)n;
         const int64_t ce = lsa ? (int64_t)n * n : n;
         if (b / per < nb && ce > key[b / per]) key[b / per] = ce;
     }
