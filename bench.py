@@ -26,6 +26,7 @@ Prints ONE JSON line on rank 0 (diagnostics go to stderr).
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import sys
@@ -573,6 +574,10 @@ def run_rank(args):
     # ragged: the assignment warm start's certified / solved counters, read
     # around the timed region (outside it)
     lsa0 = env.lsa_warm_stats() if (cfg.ragged and hasattr(env, "lsa_warm_stats")) else None
+    # no collector pass inside the timed region (a full pass over torch's
+    # object graph takes milliseconds; it would land in one step's time)
+    gc.collect()
+    gc.disable()
     if world > 1:
         dist.barrier()
     sync()
@@ -596,6 +601,7 @@ def run_rank(args):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    gc.enable()
     lsa1 = env.lsa_warm_stats() if lsa0 is not None else None
 
     # every rank's timed region; value uses the slowest (max over ranks)

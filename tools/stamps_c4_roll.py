@@ -87,5 +87,9 @@ late = np.argsort(end)[-10:]
 out["last_enders"] = [dict(w=int(i), N=int(n[i]), scn=int(scn[i]), cold=int(cold[i]), end=float(end[i]),
                            work_per_step=float(work[i] / T), wait_per_step=float((ph["grp_publish"][i] + ph["pack"][i]) / T),
                            simd_work_per_step=float(per_simd[inv[i]] / T)) for i in late]
+out["simd_work_max_over_mean"] = float(per_simd.max() / per_simd.mean())
+if os.environ.get("STAMPS_NPZ"):   # per-env arrays for offline fits of the placement cost model
+    np.savez(os.environ["STAMPS_NPZ"], scn=scn, n=n, work=work, assign=ph["assign"], physics=ph["physics"],
+             sweep=ph["sweep_publish"], cold=cold, simd_key=simd_key, end=end)
 print(json.dumps(out, indent=1))
 env.close()
