@@ -167,11 +167,17 @@ __device__ __forceinline__ uint32_t pack_lo16(uint64_t a, uint64_t b) {
 //   * the walk over each agent row's near bits counts collisions
 //     (d2 < dmin2 implies d2 < cut2) and finds coincident pairs (d2 = 0);
 //     self bits are dropped, and a wave holding a coincident pair (never
-//     seen in practice) recomputes its rows with the exact 0 < d2 <= R2.
-template <int kN, int kNo>
+//     seen in practice) recomputes its rows with the exact 0 < d2 <= R2;
+//   * kForce (fused rollout): the same walk also forms the NEXT step's
+//     contact forces — the candidates are exactly these near bits at these
+//     positions (d2 != 0), so *force = finit() (the next step's action force,
+//     formed only here so it holds no registers during the column loop) plus
+//     the contact terms in ascending collider order, the operations and order
+//     of the step kernel's force pass (bit-identical).
+template <int kN, int kNo, bool kForce = false, typename FInit = int>
 __device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, const float2 *sp, float *s_xy,
                                              float2 pm, bool full, uint64_t oo, uint64_t &row, uint64_t &cand,
-                                             int &ccnt, bool &coinc) {
+                                             int &ccnt, bool &coinc, float2 *force = nullptr, FInit finit = 0) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     constexpr int N = kN, M = kN + kNo;
     static_assert(M > 32 && M <= 64 && N <= 32 && N % 2 == 0, "one env per wave, agent bits in the low word");
@@ -256,6 +262,13 @@ __device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, 
     if (L.agent) {
         uint64_t w = near & ~(1ull << L.m);
         c = w;
+        float Fx = 0.0f, Fy = 0.0f;
+        if constexpr (kForce) {
+            const float2 f0 = finit();
+            Fx = f0.x;
+            Fy = f0.y;
+        }
+        const float dmin_aa = p.dmin_aa, dmin_ao = p.dmin_ao;   // both read before the walk
         while (w) {
             const int k = __builtin_ctzll(w);
             w &= w - 1;
@@ -266,8 +279,13 @@ __device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, 
             if (d2 == 0.0f) {
                 c &= ~(1ull << k);
                 coincident = true;
+            } else if (kForce) {
+                const float f = contact_scale(p, d2, k < N ? dmin_aa : dmin_ao);
+                Fx += f * dx;
+                Fy += f * dy;
             }
         }
+        if constexpr (kForce) *force = make_float2(Fx, Fy);
     }
     coinc = __any(coincident);   // the env (= the wave) holds a coincident pair (App. A S16)
     if (__builtin_expect(coinc, 0)) {
@@ -293,12 +311,19 @@ __device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, 
 // ccnt = collisions of agent lanes (self excluded), coinc = the lane's env
 // holds a coincident pair with an agent (d2 = 0, App. A S16). With full =
 // false the obstacle-obstacle bits are taken from `oo` (the cached masks).
-template <int kN, int kNo, int kG>
+// kForce: see obs_sweep_g1 (only with that sweep: sweep_walks_near).
+template <int kN, int kNo>
+constexpr bool sweep_walks_near(int G) {
+    return G == 1 && kN > 0 && kN <= 32 && kN % 2 == 0 && kN + kNo > 32;
+}
+template <int kN, int kNo, int kG, bool kForce = false, typename FInit = int>
 __device__ __forceinline__ void obs_sweep(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L,
                                           const float2 *sp, float *s_xy, float2 pm, bool full, uint64_t oo,
-                                          uint64_t &row, uint64_t &cand, int &ccnt, bool &coinc) {
-    if constexpr (kG == 1 && kN > 0 && kN <= 32 && kN % 2 == 0 && kN + kNo > 32) {
-        obs_sweep_g1<kN, kNo>(p, L, sp, s_xy, pm, full, oo, row, cand, ccnt, coinc);
+                                          uint64_t &row, uint64_t &cand, int &ccnt, bool &coinc,
+                                          float2 *force = nullptr, FInit finit = 0) {
+    static_assert(!kForce || sweep_walks_near<kN, kNo>(kG), "contact forces only in the near-bit walk");
+    if constexpr (sweep_walks_near<kN, kNo>(kG)) {
+        obs_sweep_g1<kN, kNo, kForce>(p, L, sp, s_xy, pm, full, oo, row, cand, ccnt, coinc, force, finit);
         return;
     }
     const int N = s.N, M = s.M;
@@ -1152,11 +1177,13 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     L0.live = L0.lane < M && L0.b < p.B;
     L0.agent = L0.live && L0.m < N;
     const int wave = L0.wave;
-    const int wstride = p.wave_lds_step + 8 * E;            // + the previous step's positions
+    // + the previous step's positions and the next step's agent forces
+    const int wstride = p.wave_lds_step + 8 * E + 8 * N;
     unsigned char *wave_lds = smem + wave * wstride;
     float2 *s_pos = (float2 *)wave_lds;
     float *s_nf = (float *)(s_pos + E);
     float2 *s_prev = (float2 *)(wave_lds + p.wave_lds_step);
+    float2 *s_force = s_prev + E;
     int *s_bc = (int *)(smem + kWavesPerBlock * wstride);   // [2][waves]: per-env edge counts by parity
     int *s_red = s_bc + 2 * kWavesPerBlock;
     const int scr_cap = (p.wave_lds_step - 8 * E) / 4;
@@ -1175,6 +1202,33 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         if (L0.lane + kWave < E) s_pos[L0.lane + kWave] = in.x1;
     }
     wave_sync();
+    // apply_environment_force: the action force plus the contact terms of the
+    // candidates in ascending collider order
+    auto add_contacts = [&](float2 F, float2 pi, uint64_t cm, const KernargParams &pc) {
+        // (both constants read before the loop: a per-lane select of the two
+        // kernarg fields compiles to a vector load and a vmcnt wait per contact)
+        const float dmin_aa = pc.dmin_aa, dmin_ao = pc.dmin_ao;
+        while (cm) {
+            const int c = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            const bool ag = c < N;
+            const float2 pj = s_pos[row_entity(c, N)];
+            const float dx = pi.x - pj.x, dy = pi.y - pj.y;
+            const float d2 = dx * dx + dy * dy;
+            const float f = contact_scale(pc, d2, ag ? dmin_aa : dmin_ao);
+            F.x += f * dx;
+            F.y += f * dy;
+        }
+        return F;
+    };
+    // With the near-bit walk (kFused) each step's sweep forms the next step's
+    // force at the positions it reads (obs_sweep_g1 kForce), so the loop runs
+    // one pass over the pairs per step; the force waits in LDS (s_force) for
+    // the next integration; the first step's force is formed here.
+    constexpr bool kFused = sweep_walks_near<kN, kNo>(1);
+    if constexpr (kFused) {
+        if (L0.agent) s_force[L0.m] = add_contacts(u, s_pos[L0.m], cand_prev, late_params());
+    }
 
     const int K = p.roll.K, n_act = p.roll.n_actions;
     const uint32_t etag = roll_epoch_tag(*p.roll.epoch);    // this launch's tag base
@@ -1251,22 +1305,15 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         KernargParams &pc = late_params();
         if (L.agent) {
             const float2 pi = s_pos[m];
-            float Fx = u.x, Fy = u.y;
-            uint64_t cm = cand_prev;
-            // (both constants read before the loop: a per-lane select of the
-            // two kernarg fields compiles to a vector load and a vmcnt wait
-            // per contact)
-            const float dmin_aa = pc.dmin_aa, dmin_ao = pc.dmin_ao;
-            while (cm) {
-                const int c = __builtin_ctzll(cm);
-                cm &= cm - 1;
-                const bool ag = c < N;
-                const float2 pj = s_pos[row_entity(c, N)];
-                const float dx = pi.x - pj.x, dy = pi.y - pj.y;
-                const float d2 = dx * dx + dy * dy;
-                const float f = contact_scale(pc, d2, ag ? dmin_aa : dmin_ao);
-                Fx += f * dx;
-                Fy += f * dy;
+            float Fx, Fy;
+            if constexpr (kFused) {
+                const float2 F = s_force[m];
+                Fx = F.x;
+                Fy = F.y;
+            } else {
+                const float2 Fc = add_contacts(u, pi, cand_prev, pc);
+                Fx = Fc.x;
+                Fy = Fc.y;
             }
             if (pc.strict && strict_bad(m, pi, N, M, [&](int c) { return s_pos[row_entity(c, N)]; })) {
                 Fx = __builtin_nanf("");
@@ -1298,7 +1345,10 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         uint64_t row, cand;
         int ccnt;
         bool coinc;
-        obs_sweep<kN, kNo, 1>(p, s, L, s_pos, s_nf, pm, false, oo, row, cand, ccnt, coinc);
+        // (kFused: the next step's force, formed by the sweep's walk)
+        auto unext = [&]() { return roll_force<kFmt>(late_params(), anext, true); };
+        float2 Fn = make_float2(0.0f, 0.0f);
+        obs_sweep<kN, kNo, 1, kFused>(p, s, L, s_pos, s_nf, pm, false, oo, row, cand, ccnt, coinc, &Fn, unext);
 
         // reward / cost
         float r = 0.0f;
@@ -1340,16 +1390,22 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             uint64_t row2, cand2;
             int cc2;
             bool coinc2;
-            obs_sweep<kN, kNo, 1>(p, s, L, s_pos, s_nf, pm2, true, 0ull, row2, cand2, cc2, coinc2);
+            float2 Fn2 = make_float2(0.0f, 0.0f);
+            obs_sweep<kN, kNo, 1, kFused>(p, s, L, s_pos, s_nf, pm2, true, 0ull, row2, cand2, cc2, coinc2, &Fn2,
+                                          unext);
             if (reset) {
                 pm = pm2;
                 row = row2;
                 cand = cand2;
                 coinc = coinc2;
+                Fn = Fn2;
             }
         }
         const bool relaid = reset;
         if (!L.live) row = 0;
+        if constexpr (kFused) {
+            if (L.agent) s_force[m] = Fn;
+        }
 
         // the step's observation outputs (node features, reward / cost above,
         // done; edges one iteration on); the simulator state (positions,
@@ -1421,7 +1477,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             if (L.lane < E) s_prev[L.lane] = s_pos[L.lane];
             if (L.lane + kWave < E) s_prev[L.lane + kWave] = s_pos[L.lane + kWave];
         }
-        u = roll_force<kFmt>(late_params(), anext, L.agent);
+        if constexpr (!kFused) u = roll_force<kFmt>(late_params(), anext, L.agent);
         arow = nrow;
         wave_sync();
     }
@@ -1494,7 +1550,7 @@ const void *roll_seg_kernel_fn(const DevParams &p, bool slots) {
     return slots ? pick_roll_seg<true>(p) : pick_roll_seg<false>(p);
 }
 size_t roll_kernel_lds(const DevParams &p) {
-    return (size_t)kWavesPerBlock * (p.wave_lds_step + 8 * p.E) + 64;
+    return (size_t)kWavesPerBlock * (p.wave_lds_step + 8 * p.E + 8 * p.N) + 64;
 }
 
 const void *emit_seg_kernel_fn(const DevParams &p) {
