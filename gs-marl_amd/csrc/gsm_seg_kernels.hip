@@ -174,8 +174,8 @@ __device__ __forceinline__ uint32_t pack_lo16(uint64_t a, uint64_t b) {
 //     formed only here so it holds no registers during the column loop) plus
 //     the contact terms in ascending collider order, the operations and order
 //     of the step kernel's force pass (bit-identical).
-template <int kN, int kNo, bool kForce = false, typename FInit = int>
-__device__ __forceinline__ void obs_sweep_g1(const DevParams &p, const Lane &L, const float2 *sp, float *s_xy,
+template <int kN, int kNo, bool kForce = false, typename FInit = int, typename Params = DevParams>
+__device__ __forceinline__ void obs_sweep_g1(const Params &p, const Lane &L, const float2 *sp, float *s_xy,
                                              float2 pm, bool full, uint64_t oo, uint64_t &row, uint64_t &cand,
                                              int &ccnt, bool &coinc, float2 *force = nullptr, FInit finit = 0) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -316,8 +316,10 @@ template <int kN, int kNo>
 constexpr bool sweep_walks_near(int G) {
     return G == 1 && kN > 0 && kN <= 32 && kN % 2 == 0 && kN + kNo > 32;
 }
-template <int kN, int kNo, int kG, bool kForce = false, typename FInit = int>
-__device__ __forceinline__ void obs_sweep(const DevParams &p, const Shape<kN, kNo> &s, const Lane &L,
+// Params: DevParams, or its kernarg view (late_params: the constants are then
+// scalar loads at the sweep, not SGPRs held across a rollout's loop)
+template <int kN, int kNo, int kG, bool kForce = false, typename FInit = int, typename Params = DevParams>
+__device__ __forceinline__ void obs_sweep(const Params &p, const Shape<kN, kNo> &s, const Lane &L,
                                           const float2 *sp, float *s_xy, float2 pm, bool full, uint64_t oo,
                                           uint64_t &row, uint64_t &cand, int &ccnt, bool &coinc,
                                           float2 *force = nullptr, FInit finit = 0) {
@@ -1156,6 +1158,11 @@ __device__ __forceinline__ float2 roll_force(const Params &p, float4 a, bool age
     return agent ? make_float2(ux * p.sens, uy * p.sens) : make_float2(0.0f, 0.0f);
 }
 
+// LDS per wave of the segmented rollout: [positions E | staging scratch 28 E]
+// rounded to 16 B, then [positions E | next forces N]
+constexpr int roll_lds_step(int E) { return (36 * E + 15) & ~15; }
+constexpr int roll_lds_wave(int N, int E) { return roll_lds_step(E) + 8 * E + 8 * N; }
+
 // kSlots: per-step outputs at base + k * stride (a rollout buffer); else every
 // step into the bound buffers (the strides are 0 and fold away)
 template <int kN, int kNo, int kFmt, bool kSlots>
@@ -1177,19 +1184,25 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     L0.live = L0.lane < M && L0.b < p.B;
     L0.agent = L0.live && L0.m < N;
     const int wave = L0.wave;
-    // + the previous step's positions and the next step's agent forces
-    const int wstride = p.wave_lds_step + 8 * E + 8 * N;
+    // Positions ping-pong between two LDS buffers: step k reads buffer k & 1
+    // and writes the agents' new positions into the other, so the previous
+    // step's positions (for its emission) need no copy; goals and obstacles
+    // (static within an episode) are kept in both. Compile-time layout
+    // (roll_kernel_lds): [positions | staging scratch], [positions | the next
+    // step's agent forces].
+    constexpr int kStep = roll_lds_step(E), wstride = roll_lds_wave(N, E);
     unsigned char *wave_lds = smem + wave * wstride;
-    float2 *s_pos = (float2 *)wave_lds;
-    float *s_nf = (float *)(s_pos + E);
-    float2 *s_prev = (float2 *)(wave_lds + p.wave_lds_step);
-    float2 *s_force = s_prev + E;
+    float2 *const s_buf0 = (float2 *)wave_lds;
+    float *s_nf = (float *)(s_buf0 + E);
+    float2 *const s_buf1 = (float2 *)(wave_lds + kStep);
+    float2 *s_force = s_buf1 + E;
+    auto pos_buf = [&](int k) { return (float2 *)(wave_lds + (k & 1) * kStep); };   // positions before step k
     int *s_bc = (int *)(smem + kWavesPerBlock * wstride);   // [2][waves]: per-env edge counts by parity
     int *s_red = s_bc + 2 * kWavesPerBlock;
-    const int scr_cap = (p.wave_lds_step - 8 * E) / 4;
+    constexpr int scr_cap = (kStep - 8 * E) / 4;
     const bool wave_live = L0.b < p.B;
     const int64_t eb = wave_live ? L0.b : 0;
-    
+
     // ---- the state before step t_first and step t_first's actions
     // (p.actions); the edges of that state were emitted by whatever ran before
     SegIn in = seg_load<kN, kNo, kFmt, true>(p, s, L0);
@@ -1198,13 +1211,13 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     float2 acc = in.acc, v = in.v, u = in.u;
     uint64_t cand_prev = in.cand_prev, oo = in.oo;
     if (wave_live) {
-        if (L0.lane < E) s_pos[L0.lane] = in.x0;
-        if (L0.lane + kWave < E) s_pos[L0.lane + kWave] = in.x1;
+        if (L0.lane < E) s_buf0[L0.lane] = s_buf1[L0.lane] = in.x0;
+        if (L0.lane + kWave < E) s_buf0[L0.lane + kWave] = s_buf1[L0.lane + kWave] = in.x1;
     }
     wave_sync();
     // apply_environment_force: the action force plus the contact terms of the
     // candidates in ascending collider order
-    auto add_contacts = [&](float2 F, float2 pi, uint64_t cm, const KernargParams &pc) {
+    auto add_contacts = [&](const float2 *s_pos, float2 F, float2 pi, uint64_t cm, const KernargParams &pc) {
         // (both constants read before the loop: a per-lane select of the two
         // kernarg fields compiles to a vector load and a vmcnt wait per contact)
         const float dmin_aa = pc.dmin_aa, dmin_ao = pc.dmin_ao;
@@ -1227,7 +1240,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     // the next integration; the first step's force is formed here.
     constexpr bool kFused = sweep_walks_near<kN, kNo>(1);
     if constexpr (kFused) {
-        if (L0.agent) s_force[L0.m] = add_contacts(u, s_pos[L0.m], cand_prev, late_params());
+        if (L0.agent) s_force[L0.m] = add_contacts(s_buf0, u, s_buf0[L0.m], cand_prev, late_params());
     }
 
     const int K = p.roll.K, n_act = p.roll.n_actions;
@@ -1272,17 +1285,19 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         // (an offset past the capacity is a legal overflow of a small slot:
         // edge_ptr keeps it, the writes below stop at the capacity)
         if (env_off < 0) {   // a broken hand-off: never write out of bounds
-            if (L.lane == 0) __hip_atomic_store((gu32 *)p.roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            env_off = p.ro.cap;
+            if (L.lane == 0)
+                __hip_atomic_store((gu32 *)late_params().roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            env_off = late_params().ro.cap;
         }
         if (wave_live) {
             KernargParams &qs = late_params();
             if (L.lane == 0) {
                 int64_t *const eptr = qs.ro.eptr + (kSlots ? (k - 1) * qs.ro.ep_s : 0);
                 eptr[L.b] = env_off;
-                if (L.b == p.B - 1) eptr[p.B] = env_off + my_cnt;
+                if (L.b == qs.B - 1) eptr[qs.B] = env_off + my_cnt;
             }
             const EdgeSink out = roll_edge_sink<kSlots>(qs, k - 1, K);
+            const float2 *s_prev = pos_buf(k);                  // positions after step t - 1
             if (staged >= 0 && env_off + staged <= out.cap)
                 write_staged<kN, kNo>(L, s_prev, (uint32_t *)s_nf, staged, env_off, out);
             else
@@ -1301,21 +1316,24 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         const int nrow = arow + 1 == n_act ? 0 : arow + 1;
         const float4 anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, ma);
 
-        // apply_environment_force + integrate_state (as gsm_step_seg_kernel)
+        // apply_environment_force + integrate_state (as gsm_step_seg_kernel):
+        // from s_cur into s_pos
+        const float2 *const s_cur = pos_buf(k);
+        float2 *const s_pos = pos_buf(k + 1);
         KernargParams &pc = late_params();
         if (L.agent) {
-            const float2 pi = s_pos[m];
+            const float2 pi = s_cur[m];
             float Fx, Fy;
             if constexpr (kFused) {
                 const float2 F = s_force[m];
                 Fx = F.x;
                 Fy = F.y;
             } else {
-                const float2 Fc = add_contacts(u, pi, cand_prev, pc);
+                const float2 Fc = add_contacts(s_cur, u, pi, cand_prev, pc);
                 Fx = Fc.x;
                 Fy = Fc.y;
             }
-            if (pc.strict && strict_bad(m, pi, N, M, [&](int c) { return s_pos[row_entity(c, N)]; })) {
+            if (pc.strict && strict_bad(m, pi, N, M, [&](int c) { return s_cur[row_entity(c, N)]; })) {
                 Fx = __builtin_nanf("");
                 Fy = __builtin_nanf("");
             }
@@ -1348,7 +1366,8 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         // (kFused: the next step's force, formed by the sweep's walk)
         auto unext = [&]() { return roll_force<kFmt>(late_params(), anext, true); };
         float2 Fn = make_float2(0.0f, 0.0f);
-        obs_sweep<kN, kNo, 1, kFused>(p, s, L, s_pos, s_nf, pm, false, oo, row, cand, ccnt, coinc, &Fn, unext);
+        obs_sweep<kN, kNo, 1, kFused>(late_params(), s, L, s_pos, s_nf, pm, false, oo, row, cand, ccnt, coinc, &Fn,
+                                      unext);
 
         // reward / cost
         float r = 0.0f;
@@ -1362,16 +1381,16 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         const int csum = wave_total(ci);
         if (L.agent) {
             KernargParams &q = late_params();
-            (q.ro.rew + (kSlots ? k * q.ro.rc_s : 0) + eb * N)[um] = p.shared_reward ? rsum : r;
+            (q.ro.rew + (kSlots ? k * q.ro.rc_s : 0) + eb * N)[um] = q.shared_reward ? rsum : r;
             (q.ro.cost + (kSlots ? k * q.ro.rc_s : 0) + eb * N)[um] = (float)ci;
         }
-        if (p.shared_reward) rsum *= (float)N;
+        if (late_params().shared_reward) rsum *= (float)N;
         if (L.live) {
             acc.x += rsum;
             acc.y += (float)csum;
         }
         bool reset = false;
-        if (done && p.auto_reset) {
+        if (done && late_params().auto_reset) {
             reset = true;
             if (m == 0) late_params().ep_last[L.b] = acc;
         }
@@ -1382,7 +1401,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
                 t = 0;
                 acc = make_float2(0.0f, 0.0f);
                 v = make_float2(0.0f, 0.0f);
-                const uint32_t gid = (uint32_t)(p.env_base + L.b);
+                const uint32_t gid = (uint32_t)(late_params().env_base + L.b);
                 for (int e = m; e < E; e += M) s_pos[e] = layout_pos(p, gid, (uint32_t)ep, (uint32_t)e);
             }
             wave_sync();
@@ -1391,8 +1410,8 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             int cc2;
             bool coinc2;
             float2 Fn2 = make_float2(0.0f, 0.0f);
-            obs_sweep<kN, kNo, 1, kFused>(p, s, L, s_pos, s_nf, pm2, true, 0ull, row2, cand2, cc2, coinc2, &Fn2,
-                                          unext);
+            obs_sweep<kN, kNo, 1, kFused>(late_params(), s, L, s_pos, s_nf, pm2, true, 0ull, row2, cand2, cc2,
+                                          coinc2, &Fn2, unext);
             if (reset) {
                 pm = pm2;
                 row = row2;
@@ -1412,7 +1431,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         // velocities, masks, counters) stays on chip and is stored once, after
         // the loop
         KernargParams &q = late_params();
-        const bool any_statics = p.nf_full || __any(relaid);
+        const bool any_statics = q.nf_full || __any(relaid);
         if (L.live) {
             float *nf = q.ro.nf + (kSlots ? k * q.ro.nf_s : 0) + eb * E * 7;
             if (L.agent) {
@@ -1449,7 +1468,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             // config's workgroup layout: with G envs per wave the last of the
             // G rollout workgroups of a slot adds the others' granules
             if (k == K - 1) {
-                const int G = p.G, r = (int)blockIdx.x;
+                const int G = q.G, r = (int)blockIdx.x;
                 if (G == 1) {
                     q.block_edge_sum[r] = sum;
                 } else {
@@ -1473,9 +1492,8 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         // keep step t for the next iteration's emission and sweep
         oo = row;
         cand_prev = L.agent ? cand : 0ull;
-        if (wave_live) {
-            if (L.lane < E) s_prev[L.lane] = s_pos[L.lane];
-            if (L.lane + kWave < E) s_prev[L.lane + kWave] = s_pos[L.lane + kWave];
+        if (__builtin_expect(relaid, 0)) {   // wave-uniform: the new episode's statics into the other buffer
+            for (int e = N + m; e < E; e += kWave) pos_buf(k)[e] = s_pos[e];
         }
         if constexpr (!kFused) u = roll_force<kFmt>(late_params(), anext, L.agent);
         arow = nrow;
@@ -1490,6 +1508,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     KernargParams &q = late_params();
     if (wave_live) {
         float2 *const pos_b = q.pos + eb * E;
+        const float2 *const s_pos = pos_buf(K);
         if (L0.lane < E) pos_b[L0.lane] = s_pos[L0.lane];
         if (L0.lane + kWave < E) pos_b[L0.lane + kWave] = s_pos[L0.lane + kWave];
         if (L0.agent) {
@@ -1550,7 +1569,7 @@ const void *roll_seg_kernel_fn(const DevParams &p, bool slots) {
     return slots ? pick_roll_seg<true>(p) : pick_roll_seg<false>(p);
 }
 size_t roll_kernel_lds(const DevParams &p) {
-    return (size_t)kWavesPerBlock * (p.wave_lds_step + 8 * p.E + 8 * p.N) + 64;
+    return (size_t)kWavesPerBlock * roll_lds_wave(p.N, p.E) + 64;
 }
 
 const void *emit_seg_kernel_fn(const DevParams &p) {
