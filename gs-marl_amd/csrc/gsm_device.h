@@ -389,7 +389,9 @@ __device__ __forceinline__ void xfer_grp_publish(const Xfer &x, uint64_t l, int 
 __device__ __forceinline__ int roll_lookback(const uint64_t *agg_k, const uint64_t *inc_k, uint32_t tag,
                                              uint32_t *status, int lane) {
     int acc = 0;
-    for (int hi = (int)blockIdx.x; hi > 0; hi -= kWave) {
+    int first = (int)blockIdx.x;
+    asm volatile("" : "+s"(first));   // no window predicates hoisted into a rollout's loop (SGPR pairs)
+    for (int hi = first; hi > 0; hi -= kWave) {
         const int idx = hi - 1 - lane;                      // lane 0 = nearest predecessor
         const int ci = idx >= 0 ? idx : 0;
         const uint64_t xi = __hip_atomic_load((const gu64 *)(inc_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

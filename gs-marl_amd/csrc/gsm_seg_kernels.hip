@@ -1198,7 +1198,8 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     float2 *s_force = s_buf1 + E;
     auto pos_buf = [&](int k) { return (float2 *)(wave_lds + (k & 1) * kStep); };   // positions before step k
     int *s_bc = (int *)(smem + kWavesPerBlock * wstride);   // [2][waves]: per-env edge counts by parity
-    int *s_red = s_bc + 2 * kWavesPerBlock;
+    int *s_red = s_bc + 2 * kWavesPerBlock;                 // [2]: the workgroup's offset (+ pad)
+    int *s_pre = s_red + 2;                                 // [2][waves]: exclusive prefix of the counts
     constexpr int scr_cap = (kStep - 8 * E) / 4;
     const bool wave_live = L0.b < p.B;
     const int64_t eb = wave_live ? L0.b : 0;
@@ -1278,8 +1279,9 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             }
         }
         __syncthreads();
-        int before = 0;
-        for (int w = 0; w < kWavesPerBlock; ++w) before += w < wave ? cb[w] : 0;
+        // (the prefix formed once by thread 0, not w < wave selects: those
+        // are loop-invariant lane masks the compiler holds in SGPR pairs)
+        const int before = s_pre[(1 - par) * kWavesPerBlock + wave];
         const int my_cnt = cb[wave];
         int64_t env_off = (int64_t)s_red[0] + before;
         // (an offset past the capacity is a legal overflow of a small slot:
@@ -1460,7 +1462,10 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         __syncthreads();
         if (threadIdx.x == 0) {
             int sum = 0;
-            for (int w = 0; w < kWavesPerBlock; ++w) sum += s_bc[par * kWavesPerBlock + w];
+            for (int w = 0; w < kWavesPerBlock; ++w) {
+                s_pre[par * kWavesPerBlock + w] = sum;
+                sum += s_bc[par * kWavesPerBlock + w];
+            }
             __hip_atomic_store((gu64 *)(q.roll.gran + (int64_t)k * gridDim.x + blockIdx.x),
                                ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)sum, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
@@ -1569,7 +1574,7 @@ const void *roll_seg_kernel_fn(const DevParams &p, bool slots) {
     return slots ? pick_roll_seg<true>(p) : pick_roll_seg<false>(p);
 }
 size_t roll_kernel_lds(const DevParams &p) {
-    return (size_t)kWavesPerBlock * roll_lds_wave(p.N, p.E) + 64;
+    return (size_t)kWavesPerBlock * roll_lds_wave(p.N, p.E) + 4 * (4 * kWavesPerBlock + 2);
 }
 
 const void *emit_seg_kernel_fn(const DevParams &p) {
