@@ -564,20 +564,23 @@ def run_rank(args):
             sync()
         if A > 0:
             capture(A, 3)
+    # no collector pass inside the timed region (a full pass over torch's
+    # object graph takes milliseconds; it would land in one step's time) —
+    # collected before the warmup: milliseconds of an idle GPU right before
+    # the timed region let its clocks drop (the driver's 20-step line measured
+    # 12.4-12.7 us/step with the collection after the warmup, same box)
+    metrics = torch.zeros(3, dtype=torch.float64, device=dev)
+    # ragged: the assignment warm start's certified / solved counters, read
+    # around the timed region (outside it)
+    lsa_stats = cfg.ragged and hasattr(env, "lsa_warm_stats")
+    gc.collect()
+    gc.disable()
     if W > 0:
         run_steps(W, 2)
     if A > 0:
         run_steps(A, 3)
+    lsa0 = env.lsa_warm_stats() if lsa_stats else None
     sync()
-    metrics = torch.zeros(3, dtype=torch.float64, device=dev)
-
-    # ragged: the assignment warm start's certified / solved counters, read
-    # around the timed region (outside it)
-    lsa0 = env.lsa_warm_stats() if (cfg.ragged and hasattr(env, "lsa_warm_stats")) else None
-    # no collector pass inside the timed region (a full pass over torch's
-    # object graph takes milliseconds; it would land in one step's time)
-    gc.collect()
-    gc.disable()
     if world > 1:
         dist.barrier()
     sync()
