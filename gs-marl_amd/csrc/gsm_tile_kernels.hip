@@ -816,6 +816,10 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
 
     // iterations 0..K-1 run step k and emit step k-1; iteration K (the tail)
     // only emits step K-1
+    // Inside the loop the launch's flags and constants are read through the
+    // kernarg view at their use (late_params()): read from `p` the compiler
+    // hoists them out of the loop and holds them in SGPRs, spilled to VGPR
+    // lanes at 8 waves per SIMD (gsm_roll_seg_kernel).
     for (int k = 0; k <= K; ++k) {
         // thread-derived values re-formed every iteration (an asm barrier): held
         // across the loop their hoisted addresses would pin VGPRs
@@ -831,7 +835,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             ep = ep + 1;
             t = 0;
             acc = make_float2(0.0f, 0.0f);
-            const uint32_t gid = (uint32_t)(p.env_base + b);
+            const uint32_t gid = (uint32_t)(late_params().env_base + b);
             __syncthreads();
             for (int e = tid; e < E; e += kTileBlock) s_pos[e] = layout_pos(p, gid, (uint32_t)ep, (uint32_t)e);
             for (int i = tid; i < N; i += kTileBlock) s_vel[i] = make_float2(0.0f, 0.0f);
@@ -844,6 +848,9 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             const float2 pi = s_pos[i];
             const float2 u = roll_action_force(late_params(), arow, eb * N + i);
             float fx = 0.0f, fy = 0.0f;
+            // (both read before the loop: a per-lane select of two kernarg
+            // fields compiles to a vector load and a vmcnt wait per contact)
+            const float dmin_aa = late_params().dmin_aa, dmin_ao = late_params().dmin_ao;
             for (int kw = 0; kw < W; ++kw) {
                 uint64_t bits = cm[(int64_t)i * W + kw];
                 while (bits) {
@@ -853,41 +860,41 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                     const float2 pj = s_pos[collider_entity(c, N)];
                     const float dx = pi.x - pj.x, dy = pi.y - pj.y;
                     const float d2 = dx * dx + dy * dy;
-                    const float f = contact_scale(p, d2, ag ? p.dmin_aa : p.dmin_ao);
+                    const float f = contact_scale(late_params(), d2, ag ? dmin_aa : dmin_ao);
                     fx += f * dx;
                     fy += f * dy;
                 }
             }
             float Fx = u.x + fx, Fy = u.y + fy;
-            if (p.strict && strict_bad(i, pi, N, p.M, [&](int c) { return s_pos[collider_entity(c, N)]; })) {
+            if (late_params().strict && strict_bad(i, pi, N, late_params().M, [&](int c) { return s_pos[collider_entity(c, N)]; })) {
                 Fx = __builtin_nanf("");
                 Fy = __builtin_nanf("");
             }
             float2 v = s_vel[i];
-            v.x = v.x * p.omd;
-            v.y = v.y * p.omd;
-            v.x = v.x + (Fx / p.mass) * p.dt;
-            v.y = v.y + (Fy / p.mass) * p.dt;
-            if (p.max_speed > 0.0f) {
+            v.x = v.x * late_params().omd;
+            v.y = v.y * late_params().omd;
+            v.x = v.x + (Fx / late_params().mass) * late_params().dt;
+            v.y = v.y + (Fy / late_params().mass) * late_params().dt;
+            if (late_params().max_speed > 0.0f) {
                 const float sp = sqrtf(v.x * v.x + v.y * v.y);
-                if (sp > p.max_speed) {
-                    v.x = v.x / sp * p.max_speed;
-                    v.y = v.y / sp * p.max_speed;
+                if (sp > late_params().max_speed) {
+                    v.x = v.x / sp * late_params().max_speed;
+                    v.y = v.y / sp * late_params().max_speed;
                 }
             }
             s_vel[i] = v;
-            s_np[i] = make_float2(pi.x + v.x * p.dt, pi.y + v.y * p.dt);
+            s_np[i] = make_float2(pi.x + v.x * late_params().dt, pi.y + v.y * late_params().dt);
         }
         __syncthreads();
         for (int i = tid; i < N; i += kTileBlock) s_pos[i] = s_np[i];
         __syncthreads();
         t += 1;
-        const bool done = t >= p.EL;
+        const bool done = t >= late_params().EL;
 
         int pairs = obs_sweep_sym(p, s_pos, sym, s_cost, eb, true, rout, rkeep, s_cm);
         auto nonfinite_part = [&]() {
             int bd = 0;
-            if (p.degenerate)
+            if (late_params().degenerate)
                 for (int i = tid; i < N; i += kTileBlock) bd |= nonfinite2(s_pos[i]) ? 1 : 0;
             return bd;
         };
@@ -901,12 +908,12 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         int cpart = 0;
         for (int i = tid; i < N; i += kTileBlock) {
             const int cnt = s_cost[i];
-            late_params().ro.cost[(kSlots ? k * p.ro.rc_s : 0) + eb * N + i] = (float)cnt;
+            late_params().ro.cost[(kSlots ? k * late_params().ro.rc_s : 0) + eb * N + i] = (float)cnt;
             cpart += cnt;
-            if (!p.shared_reward) {
+            if (!late_params().shared_reward) {
                 const float2 a = s_pos[i], g = s_pos[N + i];
                 const float dx = a.x - g.x, dy = a.y - g.y;
-                late_params().ro.rew[(kSlots ? k * p.ro.rc_s : 0) + eb * N + i] = -sqrtf(dx * dx + dy * dy);
+                late_params().ro.rew[(kSlots ? k * late_params().ro.rc_s : 0) + eb * N + i] = -sqrtf(dx * dx + dy * dy);
             }
         }
         {
@@ -931,13 +938,13 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             pairs += s_ired[kTileWaves + w];
             bad |= s_ired[2 * kTileWaves + w];
         }
-        if (p.shared_reward) {
-            for (int i = tid; i < N; i += kTileBlock) late_params().ro.rew[(kSlots ? k * p.ro.rc_s : 0) + eb * N + i] = rsum;
+        if (late_params().shared_reward) {
+            for (int i = tid; i < N; i += kTileBlock) late_params().ro.rew[(kSlots ? k * late_params().ro.rc_s : 0) + eb * N + i] = rsum;
             rsum *= (float)N;
         }
         acc.x += rsum;
         acc.y += (float)csum;
-        if (done && p.auto_reset) {
+        if (done && late_params().auto_reset) {
             if (tid == 0) late_params().ep_last[b] = acc;
             relayout();
             pairs = obs_sweep_sym(p, s_pos, sym, s_cost, eb, false, rout, rkeep, s_cm);
@@ -945,8 +952,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             bad = tile_sum(nonfinite_part(), s_ired + 3 * kTileWaves);
         }
         // the step's observation outputs: agent node rows, static rows on a new layout
-        float *nf = late_params().ro.nf + (kSlots ? k * p.ro.nf_s : 0) + eb * E * 7;
-        const bool full = relaid || p.nf_full;
+        float *nf = late_params().ro.nf + (kSlots ? k * late_params().ro.nf_s : 0) + eb * E * 7;
+        const bool full = relaid || late_params().nf_full;
         for (int i = tid; i < N; i += kTileBlock) {
             const float2 v = s_vel[i], a = s_pos[i], g = s_pos[N + i];
             float *row = nf + (int64_t)i * 7;
@@ -1004,8 +1011,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             // (an offset past the capacity is a legal overflow of a small slot:
             // edge_ptr keeps it, emit_env stops its writes at the capacity)
             if (ex < 0) {   // a broken hand-off: never write out of bounds
-                __hip_atomic_store((gu32 *)p.roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ex = (int)min(p.ro.cap, (int64_t)0x7fffffff);
+                __hip_atomic_store((gu32 *)late_params().roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                ex = (int)min(late_params().ro.cap, (int64_t)0x7fffffff);
             }
             int64_t off;
             emit_env(p, roll_edge_sink<kSlots>(late_params(), k - 1, K), s_prev, rkeep, tid == 0 ? ex : 0, &off,
@@ -1014,7 +1021,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                 KernargParams &q = late_params();
                 int64_t *const eptr = q.ro.eptr + (kSlots ? (k - 1) * q.ro.ep_s : 0);
                 eptr[b] = off;
-                if (b == p.B - 1) eptr[p.B] = off + prev_edges;
+                if (b == late_params().B - 1) eptr[late_params().B] = off + prev_edges;
             }
         }
         if (k < K) {
