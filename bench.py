@@ -248,10 +248,22 @@ def cpu_baseline(cfg, seconds, cores):
             f"pair loop), N={cfg.n_agents}, one env per process") if kind == "nav" else (
             "oracle/ragged_ref.py step over a 30-env mixed sample per process (per-env NumPy, fp64, "
             "assignment via oracle/lsa_ref.py)")
+    host = machine_cores()
     return dict(value=total / wall, unit="agent-steps/s", cores=cores, kind="port",
                 single_core_value=single, cpu_model=cpu_model(),
+                all_core=dict(value=single * host, cores=host,
+                              how=f"extrapolated: the measured mean single-process rate x the host's {host} "
+                                  "hardware threads (processes are independent envs with no shared state; a run "
+                                  "on every host core would take the other GPUs' jobs' share of the box, whose "
+                                  f"per-GPU share is the {cores} processes measured)"),
                 sample=f"{cores} host processes x {seconds:.0f} s of {what}; the reference's own CPU path is "
                        f"absent (readme.md:1)")
+
+
+def machine_cores():
+    """Hardware threads of the whole host (os.cpu_count: every CPU of the
+    machine, beyond this job's share)."""
+    return os.cpu_count() or 1
 
 
 def host_cores():
@@ -292,15 +304,22 @@ def code_object_hash(lib_path=None):
 
 
 PMC_FILE = ROOT / "profiles" / "pmc_kernels.json"
-# Instruction-issue model, measured on MI355X in the headline
-# step kernel: 200 extra independent VALU / SALU instructions per wave cost
-# 2.8 / 2.55 shader cycles each per SIMD; the shader clock under that load is
-# 2.0 GHz (s_memtime vs s_memrealtime, tools/probe_latency.hip).
-VALU_ISSUE_CYCLES = 2.8   # per wave64 VALU instruction and SIMD
-SALU_ISSUE_CYCLES = 2.55  # per SALU instruction and SIMD
-N_SIMDS = 1024            # 256 CUs x 4 SIMDs
-CLOCK_GHZ = 2.0           # measured shader clock under load
-LATENCY_BELOW = 0.6       # issue and HBM fractions both below: latency-bound
+# What binds a kernel, from its PMC counters. Issue ceilings
+# measured on MI355X (tools/probe_issue.hip, profiles/r4_probe_issue.txt:
+# every CU at 8 waves per SIMD, independent instructions): a SIMD issues at
+# most 0.447 wave64 VALU instructions per shader cycle, and a CU at most
+# 0.934 SALU instructions per cycle in total — the scalar unit is shared by
+# the CU's four SIMDs (2 waves per SIMD already saturate it), and VALU
+# instructions that write an SGPR (v_readlane) draw on the same budget. The
+# launch's own cycle count is GRBM_GUI_ACTIVE / 8 (the counter sums the 8
+# XCDs), so the fractions below are ratios within one profiled run and do not
+# depend on the bench's timing or clock.
+VALU_PEAK = 0.447     # wave64 VALU instructions per SIMD and shader cycle
+SALU_PEAK = 0.934     # SALU instructions per CU and shader cycle
+N_SIMDS = 1024        # 256 CUs x 4 SIMDs
+N_CUS = 256
+N_XCDS = 8
+BOUND_AT = 0.6        # a pipe (or HBM) above this share of its ceiling binds; none: latency-bound
 
 
 def pmc_entry(key):
@@ -361,6 +380,9 @@ def parse_args(argv=None):
                     help="two launches per step in the graphs (no lagged emission)")
     ap.add_argument("--no-roll", action="store_true",
                     help="one launch per step (lagged chain) even where a fused rollout launch exists")
+    ap.add_argument("--buffer", action="store_true",
+                    help="the training consumer: every step written to its own slot of a GraphRolloutBuffer "
+                         "(gsm_graph_capture_into: one rollout launch per episode, step k's outputs in slot k+1)")
     # launcher self-test only (tests/test_bench_launcher.py): a CPU stand-in env
     # module and gloo; the line it prints is marked as not a measurement
     ap.add_argument("--selftest-env", default=None, help=argparse.SUPPRESS)
@@ -499,6 +521,10 @@ def run_rank(args):
     env.reset(seed=cfg.seed, sync_edges=False)
 
     K, W = args.steps, args.warmup
+    if args.buffer:   # whole episodes (one buffer replay = EL steps), the episode boundary at its end
+        K = max(EL, -(-K // EL) * EL)
+        W = -(-W // EL) * EL
+        args.no_align = True
     A = 0 if args.no_align else align_steps(W, K, EL)
     chunk = min(K, EL)
     n_chunks, rem = divmod(K, chunk)
@@ -506,10 +532,26 @@ def run_rank(args):
     eager = args.eager or args.policy
     roll = not (args.unfused or args.no_roll or eager or stub)
 
+    buf = None
+    if args.buffer and not stub:
+        # the rollout buffer a runner fills: slot 0 = the episode's first
+        # observation, step k into slot k + 1 (every step at distinct addresses)
+        from gsmarl_amd import GraphRolloutBuffer
+        if args.eager or args.policy or args.no_roll or args.unfused:
+            log("error: --buffer replays the buffer's captured episode (no --eager/--policy/--no-roll/--unfused)")
+            return 2
+        buf = GraphRolloutBuffer(env, episode_length=EL)
+
     def capture(n, slot):
         """A graph of n steps: the fused rollout where the config has one
-        (n >= 2), else the lagged / two-kernel chain."""
+        (n >= 2), else the lagged / two-kernel chain. --buffer: the buffer's
+        whole episode (EL steps into its slots) whatever n is."""
         nonlocal roll
+        if buf is not None:
+            buf.capture(actions, slot=slot)
+            if not env.graph_is_rollout(slot):
+                roll = False
+            return
         if roll and n >= 2:
             try:
                 env.capture(actions, n, timing=False, slot=slot, kernels="roll")
@@ -519,8 +561,11 @@ def run_rank(args):
                 roll = False
         env.capture(actions, n, timing=False, slot=slot, kernels=gk)
 
-    settle = args.settle_ms > 0 and not eager and not stub
-    if not eager:
+    settle = args.settle_ms > 0 and not eager and not stub and buf is None
+    if buf is not None:
+        buf.reset(seed=cfg.seed)
+        capture(EL, 0)
+    elif not eager:
         if W > 0:
             capture(W, 2)
         if settle:   # slot 3 holds a whole episode first, then the alignment
@@ -549,6 +594,11 @@ def run_rank(args):
         elif args.eager:
             for t in range(n):
                 env.step(actions[t % EL], sync_edges=False)
+        elif buf is not None:
+            # the episode into the buffer's slots (the kernel launch of
+            # GraphRolloutBuffer.replay; its host-side copy of the action
+            # sequence into buf.actions is bookkeeping, left out)
+            env.replay(0)
         else:
             env.replay(slot)
 
@@ -575,7 +625,9 @@ def run_rank(args):
     lsa_stats = cfg.ragged and hasattr(env, "lsa_warm_stats")
     gc.collect()
     gc.disable()
-    if W > 0:
+    for _ in range(W // EL if buf is not None else 0):
+        run_steps(EL, 0)
+    if W > 0 and buf is None:
         run_steps(W, 2)
     if A > 0:
         run_steps(A, 3)
@@ -648,7 +700,7 @@ def run_rank(args):
     # add their own packet time to every launch.
     roofline = None
     if not args.no_kernel_timing and not eager and not stub:
-        roofline = kernel_roofline(env, cfg, actions, args, N, B, EL, roll)
+        roofline = kernel_roofline(env, cfg, actions, args, N, B, EL, roll, buf)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and not stub:
@@ -672,7 +724,10 @@ def run_rank(args):
                        "parallelism": f"env-sharded x{world} (no data-path collective)",
                        "launch": ("closed loop: GpuGraphVecEnv(output='torch', graph='coo').step(policy(obs)) "
                                   "per step, greedy on-device policy" if venv is not None else
-                                  "eager" if args.eager else (f"hip-graphs of {chunk} steps" + (
+                                  "eager" if args.eager else ("rollout buffer (GraphRolloutBuffer.capture): "
+                                  f"one launch per {EL}-step episode, step k's outputs into slot k+1 "
+                                  "(node features, rewards, costs, done, CSR edges of every step at distinct "
+                                  "addresses)" if buf is not None else "") + (f"hip-graphs of {chunk} steps" + (
                            (": all steps of a graph and their edges in one fused rollout launch (state on chip; "
                             + ("each env packs its edges a few steps behind its own step through a slab, "
                                "per-wave CSR prefix granules)" if cfg.ragged else "in-launch CSR look-back)"))
@@ -703,7 +758,53 @@ def run_rank(args):
     return 0
 
 
-def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False):
+def counter_bound(pmc, ms, hbm_frac):
+    """The roofline's counter-based figures, each a share of a
+    measured ceiling, so none exceeds 1 by more than measurement noise:
+    hbm_frac_physical = PMC HBM bytes / kernel time / 8 TB/s (what the kernel
+    moves, against `frac`, which prices the contract's algorithmic bytes);
+    valu_frac = VALU instructions / (SIMDs x launch cycles x VALU_PEAK);
+    salu_frac = SALU instructions / (CUs x launch cycles x SALU_PEAK);
+    wave_issue_frac = SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES (the share of its
+    resident time a wave spends issuing; the rest waits on memory / LDS /
+    barriers or on a busy pipe). bound: the largest of the HBM, VALU and SALU
+    shares when it reaches BOUND_AT ("hbm", or "issue" with the pipe named in
+    binding_pipe), else "latency"."""
+    out = dict(bound=None, traffic=None, hbm_frac_physical=None, valu_frac=None, salu_frac=None,
+               wave_issue_frac=None, binding_pipe=None, counters=None)
+    if not pmc:
+        return out
+    out["traffic"] = round(pmc["hbm_bytes_per_launch"])
+    hbm_phys = pmc["hbm_bytes_per_launch"] / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9)
+    out["hbm_frac_physical"] = round(hbm_phys, 4)
+    cyc = pmc.get("grbm_gui_active_per_launch")
+    shares = {"hbm": hbm_phys}
+    if cyc:
+        cyc = cyc / N_XCDS
+        vf = pmc["valu_insts_per_launch"] / (N_SIMDS * cyc * VALU_PEAK)
+        sf = pmc.get("salu_insts_per_launch", 0.0) / (N_CUS * cyc * SALU_PEAK)
+        out.update(valu_frac=round(vf, 4), salu_frac=round(sf, 4))
+        shares.update(valu=vf, salu=sf)
+    if pmc.get("wave_quad_cycles_per_launch") and pmc.get("active_inst_any_quad_cycles_per_launch"):
+        wc = pmc["wave_quad_cycles_per_launch"]
+        out["wave_issue_frac"] = round(pmc["active_inst_any_quad_cycles_per_launch"] / wc, 4)
+        waits = {k: round(pmc[f"{k}_quad_cycles_per_launch"] / wc, 4) for k in ("wait_any", "wait_inst_any")
+                 if pmc.get(f"{k}_quad_cycles_per_launch")}
+    else:
+        waits = {}
+    top = max(shares, key=shares.get)
+    out["bound"] = ("hbm" if top == "hbm" else "issue") if shares[top] >= BOUND_AT else "latency"
+    out["binding_pipe"] = top
+    w = pmc.get("waves") or 1
+    out["counters"] = dict(valu_insts_per_wave=round(pmc["valu_insts_per_launch"] / w, 1),
+                           salu_insts_per_wave=round(pmc.get("salu_insts_per_launch", 0.0) / w, 1),
+                           launch_cycles=round(cyc) if cyc else None, **waits,
+                           ceilings=f"VALU {VALU_PEAK}/SIMD/cycle, SALU {SALU_PEAK}/CU/cycle "
+                                    "(tools/probe_issue.hip), HBM 8 TB/s")
+    return out
+
+
+def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False, buf=None):
     import torch
     L = args.kernel_launches
     seg = (N + cfg.n_obstacles) <= 64 and not cfg.ragged
@@ -713,22 +814,26 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False):
     # steps, time per step — the regime of the timed region and of rocprof's
     # average (one launch from idle measured ≈7% longer: the GPU ramps); the
     # chains: event nodes around the kernel in their graph
+    if buf is not None:
+        L = EL   # the buffer's episode graph (slot 0), timed as the rollout below
     if roll:
-        env.capture(actions, L, slot=3, kernels="roll")
+        if buf is None:
+            env.capture(actions, L, slot=3, kernels="roll")
+        rs = 0 if buf is not None else 3
         # settled like the timed region (--settle-ms of back-to-back launches
         # first: timed right after the region's host-side bookkeeping, the
         # first launches ran 5% slower while the GPU ramped back up)
         t_s = time.perf_counter()
-        env.replay(3)
+        env.replay(rs)
         torch.cuda.synchronize()
         while (time.perf_counter() - t_s) * 1e3 < max(args.settle_ms, 5.0):
-            env.replay(3)
+            env.replay(rs)
             torch.cuda.synchronize()
         R = 3
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         ev0.record()
         for _ in range(R):
-            env.replay(3)
+            env.replay(rs)
         ev1.record()
         torch.cuda.synchronize()
         step_ms = ev0.elapsed_time(ev1) / R / L
@@ -754,7 +859,10 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False):
         sb = roll_step_bytes(B, N, cfg.n_obstacles, EL, 4, edges_now, seg)
         eb = emit_kernel_bytes(B, N, cfg.n_obstacles, edges_now, seg)
         fam = "seg" if seg else "tile"
-        names = (f"gsm_roll_{fam}_kernel (per step of a {L}-step launch)", f"gsm_emit_{fam}_kernel")
+        names = (f"gsm_roll_{fam}_kernel{'<slots>' if buf is not None else ''} (per step of a {L}-step launch)",
+                 f"gsm_emit_{fam}_kernel")
+        if buf is not None:   # every step's node rows in full (all E rows of every slot)
+            sb += B * (28 * (2 * N + cfg.n_obstacles - N)) * (1 - 1 / EL)
     else:
         sb = step_kernel_bytes(B, N, cfg.n_obstacles, EL, 4, seg, env.sizes.envs_per_block)
         if lag:
@@ -779,33 +887,13 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False):
     other = kern["emit" if dom == "step" else "step"]
     hbm_frac = k["gbs"] / HBM_PEAK_GBS
     pkey = f"{'roll' if (roll and dom == 'step') else 'lag' if (lag and dom == 'step') else dom}:{cfg.scenario}:N{N}:B{B}"
+    if buf is not None and dom == "step":
+        pkey = "rollbuf" + pkey[4:]
     pmc, note = pmc_entry(pkey)
-    valu = None
-    if pmc and pmc.get("valu_insts_per_launch"):
-        us = 1.0 / N_SIMDS / (CLOCK_GHZ * 1e3)   # per SIMD-cycle of the whole chip, in us
-        valu_us = pmc["valu_insts_per_launch"] * VALU_ISSUE_CYCLES * us
-        salu_us = pmc.get("salu_insts_per_launch", 0.0) * SALU_ISSUE_CYCLES * us
-        valu = dict(insts_per_launch=round(pmc["valu_insts_per_launch"]),
-                    insts_per_wave=round(pmc["valu_insts_per_launch"] / pmc["waves"], 1),
-                    salu_insts_per_wave=round(pmc.get("salu_insts_per_launch", 0.0) / pmc["waves"], 1),
-                    issue_us=round(valu_us, 3), frac=round(valu_us / (k["ms"] * 1e3), 4),
-                    issue_frac=round((valu_us + salu_us) / (k["ms"] * 1e3), 4),
-                    model=f"{VALU_ISSUE_CYCLES} / {SALU_ISSUE_CYCLES} SIMD cycles per VALU / SALU instruction "
-                          f"(measured marginal cost) x {N_SIMDS} SIMDs at {CLOCK_GHZ} GHz (DESIGN.md §5)")
-    # what binds the kernel: instruction issue (VALU + SALU) or HBM bandwidth;
-    # when neither fills even LATENCY_BELOW of its peak, one wave's dependent
-    # chain sets the time (C4's tied assignment, a lagged chain at one wave per
-    # SIMD: DESIGN.md §4/§5). achieved / frac stay the HBM figures
-    bound = "issue" if valu and valu["issue_frac"] > hbm_frac else "hbm"
-    if valu and max(valu["issue_frac"], hbm_frac) < LATENCY_BELOW:
-        bound = "latency"
-    roofline = dict(kernel=k["kernel"], bound=bound, achieved=round(k["gbs"], 1), peak=HBM_PEAK_GBS,
-                    unit="GB/s", frac=round(hbm_frac, 4), hbm_frac=round(hbm_frac, 4),
-                    valu_frac=valu["frac"] if valu else None,
-                    issue_frac=valu["issue_frac"] if valu else None,
-                    traffic=round(pmc["hbm_bytes_per_launch"]) if pmc else None,
-                    pmc=dict(key=pkey, status=note, valu=valu,
-                             source=pmc.get("source") if pmc else None),
+    roofline = dict(kernel=k["kernel"], achieved=round(k["gbs"], 1), peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=round(hbm_frac, 4), hbm_frac=round(hbm_frac, 4))
+    roofline.update(counter_bound(pmc, k["ms"], hbm_frac))
+    roofline.update(pmc=dict(key=pkey, status=note, source=pmc.get("source") if pmc else None),
                     algorithmic_bytes_per_launch=int(k["bytes"]),
                     bytes_model=bytes_model if dom == "step" else "kernel count",
                     kernel_bytes_per_launch=int(kernel_bytes) if dom == "step" else int(k["bytes"]),

@@ -9,6 +9,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <atomic>
@@ -55,6 +57,11 @@ struct gsm_handle {
     void *edge_scratch = nullptr;     // fused rollout in the bound buffers: edges of all but the last step
     void *slab = nullptr;             // ragged rollout: per-env edge slabs (depth + 1 steps)
     size_t slab_bytes = 0;
+    // the stream of the last rollout-slot launch: rollout slots share the
+    // handle's scratch (edge scratch, slabs) and state, so launches on
+    // another stream first wait for it (gsm_graph_launch)
+    hipStream_t roll_stream = nullptr;
+    bool roll_launched = false;
 };
 
 namespace {
@@ -92,7 +99,7 @@ int align16(int x) { return (x + 15) & ~15; }
 // step, linear in N_env per family. Uniform polygon / line batches put
 // polygon/line at ~63 + 27 N (tools/probe_c4_balance.py); navigation envs
 // cannot be run alone on this path, and a scan of the C4 launch time over
-// the navigation weights (tools/gpu_place_model.sh) put them at 55 + 18 N
+// the navigation weights (`tools/gpu.sh envsweep TAG c4 GSM_PLACE_MODEL ...`) put them at 55 + 18 N
 // (20 + 7 N: 39.4 us per step, 55 + 18 N: 36.9, 70 + 24 N: 38.9); padding
 // envs (b >= B) last. roll_place (gsm_ragged_kernels.hip) deals them to the
 // SIMDs in strata.
@@ -103,7 +110,7 @@ int update_block_order(gsm_handle *h, hipStream_t s) {
     const int W = (p.B + gsm::kWavesPerBlock - 1) / gsm::kWavesPerBlock * gsm::kWavesPerBlock;
     std::vector<int64_t> key(nb), cost(W, 0);
     // cost units per env and step: polygon/line a + b N, navigation c + d N,
-    // the C4 rollout's best of a scan (tools/gpu_place_model.sh,
+    // the C4 rollout's best of a scan (tools/gpu.sh envsweep,
     // GSM_PLACE_MODEL="a,b,c,d" overrides)
     int64_t ma = 63, mb = 27, mc = 55, md = 18;
     if (const char *ev = getenv("GSM_PLACE_MODEL")) {
@@ -406,6 +413,20 @@ void drop_graph(gsm_handle *h) {
 
 bool bad_slot(int32_t slot) { return slot < 0 || slot >= GSM_GRAPH_SLOTS; }
 
+// The epoch of every rollout launch in the process (DevParams::Roll::epoch):
+// one counter, started at a random point so that a granule left in device
+// memory by an earlier process does not carry the first epochs of this one.
+// A granule of launch L can match only launch L + 2^20 (gsm_device.h
+// roll_epoch_tag), whatever graph or allocation either belongs to.
+uint32_t next_launch_epoch() {
+    static std::atomic<uint32_t> next{[] {
+        uint64_t x = (uint64_t)time(nullptr) * 0x9E3779B97F4A7C15ull ^ (uint64_t)getpid() * 0xBF58476D1CE4E5B9ull;
+        x ^= x >> 31;
+        return (uint32_t)x;
+    }()};
+    return next.fetch_add(1u) & 0xfffffu;
+}
+
 // the status word is read by agent-scope loads in the kernels: cleared by the
 // same kind of stores (gsm_kernels.hip launch_granule_init), synchronously
 hipError_t clear_status(gsm_handle *h) {
@@ -706,15 +727,24 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         // the env slabs of depth + 1 steps (each env's edges at a fixed stride)
         const size_t need = (size_t)(depth + 1) * p.B * 12 * (size_t)h->sz.max_edges_per_env;
         if (h->slab_bytes < need) {
-            if (h->slab) (void)hipFree(h->slab);
-            h->slab = nullptr;
-            h->slab_bytes = 0;
-            e = hipMalloc(&h->slab, need);
+            // a deeper ring than before: the slabs are re-allocated, and every
+            // earlier ragged rollout slot is re-pointed at them (a slab holds
+            // only the edges in flight within one launch, so nothing in the
+            // old one outlives its launches: drained first)
+            void *fresh = nullptr;
+            e = hipMalloc(&fresh, need);
             if (e != hipSuccess) {
-                h->slab = nullptr;
                 if (fallback) return kRollIneligible;
                 return hip_fail(h, e, "hipMalloc (rollout edge slabs)");
             }
+            if (h->slab) {
+                e = hipDeviceSynchronize();
+                if (e != hipSuccess) { (void)hipFree(fresh); return hip_fail(h, e, "hipDeviceSynchronize (slabs)"); }
+                (void)hipFree(h->slab);
+            }
+            for (auto &o : h->slots)
+                if (o.roll && o.args.path == gsm::kPathRagged) o.args.roll.slab = (int32_t *)fresh;
+            h->slab = fresh;
             h->slab_bytes = need;
         }
     }
@@ -739,7 +769,7 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     }
     gsm_handle::Slot &sl = h->slots[slot];
     drop_slot(sl);
-    // a 16-byte header (the launch epoch), then 8-byte granules. Ragged:
+    // a 16-byte header (unused), then 8-byte granules. Ragged:
     // per-wave counts [K][xW] and group sums [K][xNG]; segmented / tile:
     // aggregates [K][nb] and inclusive prefixes [K][nb] (look-back). Zeroed
     // once here — granules are tagged with the launch epoch, so replays never
@@ -753,16 +783,12 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         if (fallback) return kRollIneligible;   // the per-step chain needs no granules
         return hip_fail(h, e, "hipMalloc (rollout granules)");
     }
-    // Every capture starts at a fresh block of 4096 launch epochs (20-bit
-    // epochs: 256 blocks before the counter wraps). A memset or store-zeroed
-    // allocation was seen to still show an agent-scope load granules left at
-    // that address by a freed graph's last replay; with consecutive start
-    // epochs those carried this graph's first tags (a freed graph replayed
-    // twice had used epochs e, e + 1; the next capture started at e + 1). No
-    // graph replayed fewer than 4096 times shares an epoch with another.
-    static std::atomic<uint32_t> next_block{0};
-    const uint32_t epoch0 = (next_block.fetch_add(1) * 4096u + 1u) & 0xfffffu;
-    e = gsm::launch_granule_init(sl.gran, gran_alloc, epoch0, h->cap_stream);
+    // Zeroed once (tag 0 never matches). Every launch then takes its own
+    // epoch (next_launch_epoch, set in gsm_graph_launch): a memset or
+    // store-zeroed allocation was seen to still show an agent-scope load
+    // granules left at that address by a freed graph's last replay, and with
+    // per-capture epochs those could carry this graph's tags.
+    e = gsm::launch_granule_init(sl.gran, gran_alloc, 0u, h->cap_stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->cap_stream);
     if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "rollout granule init"); }
     const bool ends = (flags & GSM_GRAPH_TIME_ENDS) != 0;
@@ -795,9 +821,15 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     const int place_S = 4 * n_cu;
     int place_R = 0;
     if (ragged && h->place_order && xW % place_S == 0) place_R = xW / place_S;
-    if (const char *ev = getenv("GSM_ROLL_PLACE")) if (atoi(ev) == 0) place_R = 0;
+    // (GSM_ROLL_PLACE=2, a test knob: every wave registers, then the launch
+    // decides identity, the partial-residency fallback)
+    int place_force = 0;
+    if (const char *ev = getenv("GSM_ROLL_PLACE")) {
+        if (atoi(ev) == 0) place_R = 0;
+        if (atoi(ev) == 2) place_force = 1;
+    }
     p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, xW, xNG, depth,
-                                  h->sz.max_edges_per_env, place_R, sl.gran + 2, h->roll_status, (uint32_t *)sl.gran,
+                                  h->sz.max_edges_per_env, place_R, sl.gran + 2, h->roll_status, 0u, place_force,
                                   (int32_t *)h->slab, place_R ? h->place_order : nullptr, place_S, 0};
     if (e == hipSuccess) {
         what = "rollout kernel node";
@@ -1026,8 +1058,17 @@ int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream) {
     if (sl.direct) {   // a rollout graph: its one kernel, launched directly
         // (GSM_GRAPH_TIME_ENDS: events recorded on the stream around it — as
         // graph event nodes they added ≈7% to the launch they bracketed)
+        hipError_t e = hipSuccess;
+        // rollout launches of one handle never overlap: they share its
+        // scratch and state (a launch on another stream first waits for the
+        // previous stream's work)
+        if (h->roll_launched && h->roll_stream != as_stream(stream)) e = hipStreamSynchronize(h->roll_stream);
+        if (e != hipSuccess) return hip_fail(h, e, "hipStreamSynchronize (previous rollout stream)");
+        h->roll_stream = as_stream(stream);
+        h->roll_launched = true;
+        sl.args.roll.epoch = next_launch_epoch();   // copied with the arguments at the launch
         void *args[] = {&sl.args};
-        hipError_t e = sl.events.empty() ? hipSuccess : hipEventRecord(sl.events.front(), as_stream(stream));
+        e = sl.events.empty() ? hipSuccess : hipEventRecord(sl.events.front(), as_stream(stream));
         if (e == hipSuccess) e = hipLaunchKernel(sl.fn, sl.grid, sl.block, args, sl.lds, as_stream(stream));
         if (e == hipSuccess && !sl.events.empty()) e = hipEventRecord(sl.events.back(), as_stream(stream));
         if (e != hipSuccess) return hip_fail(h, e, "hipLaunchKernel (rollout)");

@@ -280,17 +280,16 @@ __device__ __forceinline__ float2 roll_action_force(const Params &p, int row, in
 // ---- granule tags of the rollouts' CSR hand-offs
 // A granule is 8 bytes {tag32 << 32 | value32}, stored and loaded with relaxed
 // agent-scope atomics (write-through, no fence). tag32 = epoch20 << 12 |
-// (step + 1): the launch epoch (20 bits; read from the graph's epoch word at
-// launch start, advanced in-kernel once every wave / workgroup has read it)
-// and the step within the launch (K <= kRollMaxSteps). Every capture starts
-// at a fresh block of 4096 epochs (gsm_abi.hip), so no granule left in memory
-// by an earlier launch — of this graph, or of a graph freed before this one
-// was allocated at the same address — carries a tag of this launch (observed
-// otherwise: a memset / store-initialised allocation still showed an
-// agent-scope load the granules of the previous graph's last replay). Tag 0
-// is never valid (step + 1 >= 1), so zeroed memory never matches.
+// (step + 1): the launch epoch (20 bits, DevParams::Roll::epoch: assigned by
+// the host to every launch from one process-wide counter) and the step within
+// the launch (K <= kRollMaxSteps). No granule left in memory by another
+// launch — of this graph, or of a graph freed before this one was allocated
+// at the same address — carries a tag of this launch until 2^20 launches
+// later (observed before per-launch epochs: a memset / store-initialised
+// allocation still showed an agent-scope load the granules of the previous
+// graph's last replay). Tag 0 is never valid (step + 1 >= 1), so zeroed
+// memory never matches.
 __device__ __forceinline__ uint32_t roll_epoch_tag(uint32_t epoch) { return (epoch & 0xfffffu) << 12; }
-__device__ __forceinline__ uint32_t roll_next_epoch(uint32_t epoch) { return (epoch + 1u) & 0xfffffu; }
 
 // ---- per-wave CSR hand-off of the one-env-per-wave rollouts
 // (the ragged rollout, gsm_ragged_kernels.hip; `depth` = the lag between a

@@ -91,16 +91,17 @@ struct DevParams {
     // gsm_roll_tile_kernel). Iteration k runs step t_first + k with the
     // actions at actions + ((t_first + k) % n_actions) * stride and emits the
     // edges of an earlier step (ro); the tail after the loop emits the last.
-    // The CSR prefix of step t crosses waves / workgroups through `gran`,
-    // after a 16-byte header holding the launch epoch. Granules are 8-byte
-    // {tag32, value32} (gsm_device.h roll_epoch_tag: 20-bit epoch, 12-bit
-    // step): the ragged rollout's per-wave counts and group sums (Xfer,
-    // packing `depth` steps behind), the seg / tile rollouts' workgroup
-    // aggregates [K][grid] then inclusive prefixes [K][grid] (decoupled
-    // look-back). The epoch is advanced by the launch's last wave / workgroup
-    // once every one has read it, so no granule is ever cleared between
-    // launches; each capture starts at a fresh block of 4096 epochs. `status` is set when
-    // a bounded wait gave up.
+    // The CSR prefix of step t crosses waves / workgroups through `gran`.
+    // Granules are 8-byte {tag32, value32} (gsm_device.h roll_epoch_tag:
+    // 20-bit launch epoch, 12-bit step): the ragged rollout's per-wave counts
+    // and group sums (Xfer, packing `depth` steps behind), the seg / tile
+    // rollouts' workgroup aggregates [K][grid] then inclusive prefixes
+    // [K][grid] (decoupled look-back). `epoch` is assigned by the host to
+    // every launch from one process-wide counter (gsm_abi.hip
+    // next_launch_epoch), so no granule is ever cleared between launches and
+    // no granule left by another launch — of this graph or of any graph whose
+    // allocation this one reuses — carries this launch's tag. `status` is set
+    // when a bounded wait gave up.
     struct Roll {
         const char *actions;
         int64_t stride;
@@ -111,7 +112,8 @@ struct DevParams {
         int32_t place_R;      // ragged rollout placement: waves per SIMD when the grid fills every SIMD
         uint64_t *gran;
         uint32_t *status;
-        uint32_t *epoch;
+        uint32_t epoch;       // this launch's epoch (20 bits), set per launch by gsm_graph_launch
+        int32_t place_force;  // test knob (GSM_ROLL_PLACE=2): register, then decide identity
         int32_t *slab;        // ragged rollout: [depth + 1][B] slabs of [2][slab_e] int32 + [slab_e] f32
         const int32_t *place; // ragged rollout: [W] envs by descending cost (nullptr: env = wave index)
         int32_t place_S, pad; // SIMDs the grid fills (place_R * place_S = W)

@@ -1079,13 +1079,21 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_ragged_kernel(DevParams p) {
 // within kPlaceWaitTicks and exactly place_S SIMDs hold them with no SIMD
 // above place_R -> dealt; else (another kernel holds CUs: partial
 // residency) env = wave index, whose waits are on earlier-dispatched waves
-// only. Registration uses returning atomics only (each completes before the
-// next is issued) on words tagged with this launch's epoch, so nothing needs
-// clearing except the arrival / SIMD counters, which the epoch bumper zeroes
-// at the end of the launch; a wrong decision cannot go unnoticed (every env
-// is claimed by a tagged exchange: a second claim sets status 4, a missing
-// env times its successors out).
-constexpr uint64_t kPlaceWaitTicks = 40000;   // 400 us of s_memrealtime
+// only. The decision is identity as soon as the arrival count has not grown
+// for kPlaceStallTicks (the non-resident workgroups cannot arrive before the
+// resident ones finish), at the latest after kPlaceWaitTicks. Registration
+// uses returning atomics only, each wave waits for its own (and makes them
+// visible at agent scope) before the workgroup barrier that precedes the
+// arrival count, and the deciding wave acquires after it has seen every
+// arrival; the words are tagged with this launch's epoch, so nothing needs
+// clearing except the arrival / SIMD counters, which the grid's last wave
+// zeroes at the end of the launch. A wrong decision cannot go unnoticed:
+// every env is claimed by a tagged exchange (a second claim sets status 4, a
+// missing env times its successors out), and a dealt slot outside the
+// placement table (r >= place_R, i >= place_S, env >= the grid's waves) sets
+// status 5 and runs the wave's own index instead of reading past the table.
+constexpr uint64_t kPlaceWaitTicks = 40000;    // 400 us of s_memrealtime
+constexpr uint64_t kPlaceStallTicks = 5000;    // 50 us without a new arrival
 constexpr uint32_t kPlaceIdentity = 1, kPlaceDealt = 2;
 __device__ __forceinline__ uint64_t place_ld(const uint64_t *g) {   // a wave-uniform atomic load
     const uint64_t x = __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1109,7 +1117,7 @@ __device__ int roll_place(const int wg_wave, const uint32_t epoch) {
     const int key = (int)((grp << 7) | (((hw >> 12) & 1u) << 6) | (((hw >> 8) & 15u) << 2) | ((hw >> 4) & 3u));
     const uint32_t slot = hw & 15u;
     const int R = q.roll.place_R, S = q.roll.place_S;
-    if (lane == 0) {   // returning atomics only: each completes before the next is issued
+    if (lane == 0) {   // returning atomics only (results used): each completes before the next is issued
         gu64 *mk = (gu64 *)(A + PlaceArea::kMask + key);
         uint64_t x = __hip_atomic_load(mk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), have;
         for (;;) {
@@ -1119,20 +1127,27 @@ __device__ int roll_place(const int wg_wave, const uint32_t epoch) {
                 break;
         }
         const int before = __popc((uint32_t)have);
+        uint64_t sink = 0;
         if (before == 0) {   // the SIMD's first wave: its index within the group
             const uint64_t il = __hip_atomic_fetch_add((gu64 *)(A + PlaceArea::kNsimd + 8 * grp), 1ull,
                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            (void)__hip_atomic_exchange((gu64 *)(A + PlaceArea::kRank + key), (uint64_t)ptag << 32 | (uint32_t)il,
-                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sink ^= __hip_atomic_exchange((gu64 *)(A + PlaceArea::kRank + key), (uint64_t)ptag << 32 | (uint32_t)il,
+                                          __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         if (before + 1 > R)
-            (void)__hip_atomic_exchange((gu64 *)(A + PlaceArea::kBad), (uint64_t)ptag << 32, __ATOMIC_RELAXED,
-                                        __HIP_MEMORY_SCOPE_AGENT);
+            sink ^= __hip_atomic_exchange((gu64 *)(A + PlaceArea::kBad), (uint64_t)ptag << 32, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(sink));   // the returned values are used: returning atomics
     }
+    // each wave's registration complete and visible at agent scope before the
+    // workgroup's arrival is counted
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();   // the workgroup's waves have registered: one arrival for all four
-    if (threadIdx.x == 0)
-        (void)__hip_atomic_fetch_add((gu64 *)(A + PlaceArea::kArrive + 8 * grp), 1ull, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+        const uint64_t o = __hip_atomic_fetch_add((gu64 *)(A + PlaceArea::kArrive + 8 * grp), 1ull,
+                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(o));
+    }
     // The decision, by workgroup 0's first wave (dispatched first, so always
     // resident): it polls the arrival counters and publishes to one replica
     // of the decision per counter group; every other wave polls its group's
@@ -1141,26 +1156,38 @@ __device__ int roll_place(const int wg_wave, const uint32_t epoch) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint32_t dec = 0;
     if (wg_wave == 0) {
+        int seen = -1;
+        uint64_t t_seen = t0;
         for (;;) {
             const uint64_t a = __hip_atomic_load((gu64 *)(A + PlaceArea::kArrive + 8 * lane), __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_AGENT);
             const int arrived = wave_total((int)a);
-            const uint64_t dt = __builtin_amdgcn_s_memrealtime() - t0;
+            const uint64_t tn = __builtin_amdgcn_s_memrealtime();
             if (arrived == (int)gridDim.x) {
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every registration before the reads below
                 const uint64_t n = __hip_atomic_load((gu64 *)(A + PlaceArea::kNsimd + 8 * lane), __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT);
                 const uint64_t bad = place_ld(A + PlaceArea::kBad);
-                dec = (wave_total((int)n) == S && (uint32_t)(bad >> 32) != ptag) ? kPlaceDealt : kPlaceIdentity;
+                dec = (wave_total((int)n) == S && (uint32_t)(bad >> 32) != ptag && !q.roll.place_force)
+                          ? kPlaceDealt : kPlaceIdentity;
                 break;
             }
-            if (dt > kPlaceWaitTicks) {
+            if (arrived != seen) {
+                seen = arrived;
+                t_seen = tn;
+            }
+            // partial residency: the arrivals stopped (the rest are waiting
+            // for resident workgroups to finish), or the outer bound
+            if (tn - t_seen > kPlaceStallTicks || tn - t0 > kPlaceWaitTicks) {
                 dec = kPlaceIdentity;
                 break;
             }
             __builtin_amdgcn_s_sleep(2);
         }
-        (void)__hip_atomic_exchange((gu64 *)(A + PlaceArea::kMode + 8 * lane), (uint64_t)ptag << 32 | dec,
-                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t o = __hip_atomic_exchange((gu64 *)(A + PlaceArea::kMode + 8 * lane),
+                                                 (uint64_t)ptag << 32 | dec, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(o));
     } else {
         for (;;) {
             const uint64_t m = place_ld(A + PlaceArea::kMode + 8 * grp);
@@ -1195,10 +1222,21 @@ __device__ int roll_place(const int wg_wave, const uint32_t epoch) {
     }
     const uint64_t nx = lane < (int)grp ? __hip_atomic_load((gu64 *)(A + PlaceArea::kNsimd + 8 * lane),
                                                             __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
-    const int i = (int)(uint32_t)rk + wave_total((int)nx);
+    const int i = __builtin_amdgcn_readfirstlane((int)(uint32_t)rk + wave_total((int)nx));
     const int r = __popc((uint32_t)mk & ((1u << slot) - 1u));
+    // a dealt slot is inside the table by construction (exactly S SIMDs, none
+    // above R waves); checked anyway, so that a wrong decision can never read
+    // past the table or run an env index outside the grid
+    if (r >= R || i < 0 || i >= S) {
+        if (lane == 0) __hip_atomic_store((gu32 *)q.roll.status, 5u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return wg_wave;
+    }
     const int pos = r * S + ((r & 1) ? S - 1 - i : i);
     const int env = __builtin_amdgcn_readfirstlane(q.roll.place[pos]);
+    if (env < 0 || env >= q.roll.xW) {
+        if (lane == 0) __hip_atomic_store((gu32 *)q.roll.status, 5u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return wg_wave;
+    }
     if (lane == 0) {
         const uint32_t old = __hip_atomic_exchange((gu32 *)((uint32_t *)(A + PlaceArea::kClaim) + env), ptag,
                                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1218,7 +1256,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const uint32_t epoch = *p.roll.epoch;
+    const uint32_t epoch = p.roll.epoch;
     // the env this wave runs (SIMD-balanced placement, or the wave's index)
     const int w = __builtin_amdgcn_readfirstlane(roll_place((int)blockIdx.x * kWavesPerBlock + wave, epoch));
     const int Nmax = p.N, Tmax = p.T, Emax = p.E;
@@ -1569,14 +1607,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         ring = ring == D ? 0 : ring + 1;
     }
     // The grid's last wave has read (directly or through the group sums) a
-    // granule of this launch from every wave: advance the epoch.
-    if (w == xf().W - 1 && lane == 0) {
-        KernargParams &q = late_params();
-        __hip_atomic_store((gu32 *)q.roll.epoch, roll_next_epoch(epoch), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // every wave has registered and decided: the placement counters for the
-    // next launch (one per lane), and this launch's decision counted
+    // granule of this launch from every wave, so every wave has registered
+    // and decided: the placement counters for the next launch (one per lane),
+    // and this launch's decision counted
     if (w == xf().W - 1 && late_params().roll.place) {
         KernargParams &q = late_params();
         uint64_t *const A = place_area(q);

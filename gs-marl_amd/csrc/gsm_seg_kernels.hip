@@ -1245,7 +1245,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     }
 
     const int K = p.roll.K, n_act = p.roll.n_actions;
-    const uint32_t etag = roll_epoch_tag(*p.roll.epoch);    // this launch's tag base
+    const uint32_t etag = roll_epoch_tag(p.roll.epoch);     // this launch's tag base
     int arow = p.roll.t_first % n_act;                      // action row of the current step
     uint8_t deg = 0;                                        // App. A S16 flags of the final state
     // The edges of step t_first + k - 1, emitted in iteration k (k = 1..K-1)
@@ -1269,13 +1269,6 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
                                    ((uint64_t)(etag | (uint32_t)k) << 32) |
                                        (uint32_t)(ex + cb[0] + cb[1] + cb[2] + cb[3]),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                // After the tail's look-back of the LAST workgroup every
-                // workgroup has published a granule of this launch, so all
-                // have read the epoch: advance it for the next launch
-                // (granules are never cleared; a stale one cannot match).
-                if (k == K && blockIdx.x == gridDim.x - 1)
-                    __hip_atomic_store((gu32 *)qe.roll.epoch, roll_next_epoch(etag >> 12), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         __syncthreads();

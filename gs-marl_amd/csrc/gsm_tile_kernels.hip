@@ -809,7 +809,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     float2 acc = p.ep_acc[b];
     if (tid == 0) s_deg[0] = s_deg[1] = 0;
     const int K = p.roll.K, n_act = p.roll.n_actions;
-    const uint32_t etag = roll_epoch_tag(*p.roll.epoch);    // this launch's tag base
+    const uint32_t etag = roll_epoch_tag(p.roll.epoch);     // this launch's tag base
     int arow = p.roll.t_first % n_act;
     int prev_edges = 0, bad = 0;
     __syncthreads();
@@ -1001,11 +1001,6 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                                        ((uint64_t)(etag | (uint32_t)k) << 32) | (uint32_t)(ex + prev_edges),
                                        __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
-                    // the tail's look-back of the last workgroup: every
-                    // workgroup has read the epoch (gsm_roll_seg_kernel)
-                    if (k == K && b == (int)gridDim.x - 1)
-                        __hip_atomic_store((gu32 *)q.roll.epoch, roll_next_epoch(etag >> 12), __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
                 }
             }
             // (an offset past the capacity is a legal overflow of a small slot:

@@ -292,6 +292,12 @@ int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t 
  * launch writing step j's outputs into slot j; else the per-step chain. */
 int gsm_graph_capture_into(gsm_handle *h, int32_t slot, const void *actions, int64_t action_stride_bytes,
                            int32_t n_actions, int32_t n_steps, int action_fmt, const gsm_outputs *per_step);
+/* Launch the graph in `slot` on `stream` (stream-ordered, asynchronous). A
+ * rollout slot (GSM_GRAPH_ROLL, or a rollout buffer's single launch) is its one
+ * kernel launched directly, with a fresh launch epoch for its hand-off tags;
+ * the rollout slots of a handle share its state and scratch, so their launches
+ * never overlap: a launch on a different stream than the handle's previous
+ * rollout launch first waits for that stream (host-side synchronisation). */
 int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream);
 /* The graph in `slot`: its step count (0 if none) and whether it is one
  * fused rollout launch (GSM_GRAPH_ROLL, or gsm_graph_capture_into on a
@@ -299,8 +305,10 @@ int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream);
 int gsm_graph_info(gsm_handle *h, int32_t slot, int32_t *steps, int32_t *fused);
 /* After graph launches have completed: *gave_up = 1 if any bounded in-launch
  * wait (a rollout launch's CSR hand-off, or the ragged lagged chain's staging
- * wait) timed out since the last call (that launch's edges are then invalid),
- * else 0. Clears the flag. Synchronises (reads a device word). */
+ * wait) timed out, or an in-launch check failed (an out-of-range CSR offset,
+ * a doubly claimed env, a placement slot outside its table), since the last
+ * call (that launch's outputs are then invalid), else 0. Clears the flag.
+ * Synchronises (reads a device word). */
 int gsm_graph_roll_status(gsm_handle *h, int32_t *gave_up);
 /* Ragged mixed rollouts deal their envs to the SIMDs by estimated cost when
  * every wave of the launch is resident (else env = wave index; same outputs

@@ -223,9 +223,8 @@ def test_roll_recycled_granules(N, B, T, mode):
     an agent-scope load may still see after the new allocation is zeroed (a
     hipMemset's zeros did not hide them: the second env of a pair got the
     first's group sums). Each graph is replayed three times before it is
-    freed (its in-kernel epoch advances per replay); every capture starts at
-    a fresh block of epochs, so no left-over granule carries a tag of the
-    next graph's launches."""
+    freed; every launch takes its own epoch from one process-wide counter,
+    so no left-over granule carries a tag of the next graph's launches."""
     from gsmarl_amd import GraphRolloutBuffer
     for rep in range(3):
         env, cfg = _env(n_agents=N, n_envs=B, seed=2, episode_length=6)
@@ -258,3 +257,35 @@ def test_roll_recycled_granules(N, B, T, mode):
         assert not env.roll_gave_up()
         env.close()
         ref.close()
+
+
+def test_roll_recycled_after_many_replays():
+    """A graph replayed more than 4096 times (the per-capture epoch blocks of
+    round 3 ran into the next capture's block there), freed, and a new
+    capture at the recycled granule allocation: the new graph still equals
+    eager steps, and no bounded wait gives up."""
+    N, B, T = 3, 100, 2
+    env, _ = _env(n_agents=N, n_envs=B, seed=4, episode_length=6)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    env.reset(seed=4)
+    env.capture(acts, T, slot=0, kernels="roll")
+    for _ in range(4200):
+        env.replay(0)
+    torch.cuda.synchronize()
+    assert not env.roll_gave_up()
+    env.close()
+    env, _ = _env(n_agents=N, n_envs=B, seed=4, episode_length=6)
+    ref, _ = _env(n_agents=N, n_envs=B, seed=4, episode_length=6)
+    env.reset(seed=4)
+    env.capture(acts, T, slot=0, kernels="roll")
+    env.replay(0)
+    ref.reset(seed=4)
+    for t in range(T):
+        ref.step(acts[t], sync_edges=False)
+    torch.cuda.synchronize()
+    assert not env.roll_gave_up()
+    assert torch.equal(env.t["edge_ptr"], ref.t["edge_ptr"])
+    n = int(ref.t["edge_ptr"][-1])
+    assert torch.equal(env.t["edge_index"][..., :n], ref.t["edge_index"][..., :n])
+    env.close()
+    ref.close()

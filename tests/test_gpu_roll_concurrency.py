@@ -78,3 +78,37 @@ def test_roll_with_cus_taken(kind):
         print(f"placement: dealt {dealt}, fell back {fell_back}")
         assert dealt + fell_back == 1
     env.close()
+
+
+def test_roll_ragged_forced_identity(monkeypatch):
+    """The partial-residency fallback exercised deterministically: with the
+    test knob GSM_ROLL_PLACE=2 every wave registers, the launch then decides
+    env = wave index (as it does when the arrivals stall); the outputs equal
+    eager steps bit for bit and the launch is counted as fallen back."""
+    kw = dict(n_agents=24, n_envs=8192, seed=5, episode_length=100, scenario="mixed", n_agents_min=3)
+    env = _env(**kw)
+    T = 12
+    acts = torch.randint(0, 5, (T, 8192, 24), dtype=torch.int32, device=DEV)
+    _reset(env, 5, True)
+    for t in range(T):
+        env.step(acts[t], sync_edges=False)
+    torch.cuda.synchronize()
+    ref = {k: v.clone() for k, v in env.t.items()}
+    _reset(env, 5, True)
+    monkeypatch.setenv("GSM_ROLL_PLACE", "2")
+    env.capture(acts, T, slot=0, kernels="roll")   # the knob is read at capture
+    monkeypatch.delenv("GSM_ROLL_PLACE")
+    assert env.graph_is_rollout(0)
+    env.roll_placement()   # clear the counts
+    env.replay(0)
+    torch.cuda.synchronize()
+    assert not env.roll_gave_up()
+    n = int(ref["edge_ptr"][-1])
+    for k in ref:
+        if k in ("edge_index", "edge_attr"):
+            assert torch.equal(ref[k][..., :n], env.t[k][..., :n]), k
+        else:
+            assert torch.equal(ref[k], env.t[k]), k
+    dealt, fell_back = env.roll_placement()
+    assert (dealt, fell_back) == (0, 1)
+    env.close()

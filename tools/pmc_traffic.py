@@ -15,6 +15,7 @@ bench.py compares it with the launch time per step.
 Usage: python tools/pmc_traffic.py OUT_JSON [KINDS@]KEY_PREFIX=SUMMARY_DIR ...
   e.g. h:navigation:N24:B8192=gpurun_out/pmc_h  (keys: step:navigation:N24:B8192, emit:...)
        lag@h:navigation:N24:B8192=gpurun_out/pmc_h_lag  (only the lagged step kernel)
+       roll>rollbuf@b:navigation:N24:B8192=...  (the rollout kernel, stored as rollbuf:navigation:...)
 """
 import json
 import os
@@ -36,9 +37,15 @@ ent = res.setdefault("entries", {})
 for spec in sys.argv[2:]:
     key, d = spec.split("=", 1)
     kinds = None
+    rename = {}
     if "@" in key:
         k0, key = key.split("@", 1)
-        kinds = set(k0.split("+"))
+        kinds = set()
+        for kk in k0.split("+"):   # "roll>rollbuf": kernel roll stored under the name rollbuf
+            src, _, dst = kk.partition(">")
+            kinds.add(src)
+            if dst:
+                rename[src] = dst
     txt = open(os.path.join(d, "summary.txt")).read()
     summ = json.loads(txt[txt.index("{"):])
     for kern, v in summ.items():
@@ -52,18 +59,21 @@ for spec in sys.argv[2:]:
         e = dict(hbm_bytes_per_launch=round(rd + wr), read_bytes_corrected=round(rd), write_bytes=round(wr),
                  fetch_size_kib=c["FETCH_SIZE"], write_size_kib=c["WRITE_SIZE"], dispatches=v["dispatches"],
                  source=d)
-        for cn, k in (("SQ_INSTS_VALU", "valu_insts_per_launch"), ("SQ_INSTS_SALU", "salu_insts_per_launch"),
-                      ("SQ_INSTS_LDS", "lds_insts_per_launch"), ("SQ_WAVES", "waves"),
-                      ("SQ_WAVE_CYCLES", "wave_quad_cycles_per_launch")):
+        PER_LAUNCH = (("SQ_INSTS_VALU", "valu_insts_per_launch"), ("SQ_INSTS_SALU", "salu_insts_per_launch"),
+                      ("SQ_INSTS_LDS", "lds_insts_per_launch"), ("SQ_WAVE_CYCLES", "wave_quad_cycles_per_launch"),
+                      ("SQ_ACTIVE_INST_ANY", "active_inst_any_quad_cycles_per_launch"),
+                      ("SQ_WAIT_ANY", "wait_any_quad_cycles_per_launch"),
+                      ("SQ_WAIT_INST_ANY", "wait_inst_any_quad_cycles_per_launch"),
+                      ("GRBM_GUI_ACTIVE", "grbm_gui_active_per_launch"))
+        for cn, k in PER_LAUNCH + (("SQ_WAVES", "waves"),):
             if cn in c:
                 e[k] = c[cn]
         if kern == "roll":   # per step of the launch
             n = int(os.environ.get("ROLL_STEPS", "100"))
-            for k in ("hbm_bytes_per_launch", "read_bytes_corrected", "write_bytes", "valu_insts_per_launch",
-                      "salu_insts_per_launch", "lds_insts_per_launch", "wave_quad_cycles_per_launch"):
+            for k in ("hbm_bytes_per_launch", "read_bytes_corrected", "write_bytes") + tuple(k for _, k in PER_LAUNCH):
                 if k in e:
                     e[k] = round(e[k] / n, 1)
             e["per"] = f"step (counters of one {n}-step launch / {n})"
-        ent[f"{kern}:{key.split(':', 1)[1]}"] = e
+        ent[f"{rename.get(kern, kern)}:{key.split(':', 1)[1]}"] = e
 json.dump(res, open(out_path, "w"), indent=1, sort_keys=True)
 print(json.dumps(res, indent=1))
