@@ -62,6 +62,10 @@ struct gsm_handle {
     // another stream first wait for it (gsm_graph_launch)
     hipStream_t roll_stream = nullptr;
     bool roll_launched = false;
+    // gsm_step as a one-step rollout launch (step + its edges in one kernel):
+    // -1 not yet decided for this config, 0 no (two launches), 1 yes
+    int eager_roll = -1;
+    uint64_t *eager_gran = nullptr;   // its granules (K = 1)
 };
 
 namespace {
@@ -369,6 +373,59 @@ int redirect(gsm_handle *h, gsm::DevParams *p, const gsm_outputs *o) {
     return GSM_OK;
 }
 
+uint32_t next_launch_epoch();
+hipError_t clear_status(gsm_handle *h);
+
+// gsm_step as ONE launch: the config's fused rollout kernel with K = 1 (the
+// step, then its edges at the CSR offset of the in-launch look-back) instead
+// of the step kernel + the emit kernel — the same operations, so the same
+// outputs (tests/test_gpu_roll.py compares the rollout with the two-kernel
+// chain step for step). Segmented configs with a compiled rollout shape and
+// the tile path, when the grid fits one residency round (decided once per
+// handle). The ragged path keeps its two launches (a rollout launch there
+// runs the SIMD placement and the per-env slabs, built for long launches).
+// GSM_EAGER_TWO_KERNELS=1 selects the two launches everywhere.
+constexpr int kEagerIneligible = 1;
+int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
+    if (h->eager_roll == 0 || p.path == gsm::kPathRagged) return kEagerIneligible;
+    const bool tile = p.path == gsm::kPathTile;
+    const void *fn = tile ? gsm::roll_tile_kernel_fn(p, false) : gsm::roll_seg_kernel_fn(p, false);
+    if (!fn) return kEagerIneligible;   // (the action format may differ per call: checked every time)
+    const int nb = tile ? gsm::step_grid_blocks(p) : (p.B + gsm::kWavesPerBlock - 1) / gsm::kWavesPerBlock;
+    const size_t lds = tile ? gsm::roll_tile_kernel_lds(p) : gsm::roll_kernel_lds(p);
+    if (h->eager_roll < 0) {
+        h->eager_roll = 0;
+        if (const char *ev = getenv("GSM_EAGER_TWO_KERNELS")) if (atoi(ev) != 0) return kEagerIneligible;
+        int dev = 0, per_cu = 0, n_cu = 0;
+        hipError_t e = hipGetDevice(&dev);
+        if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+        if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, gsm::block_threads(p), lds);
+        if (e != hipSuccess) return hip_fail(h, e, "occupancy query (eager rollout)");
+        if ((int64_t)per_cu * n_cu < nb) return kEagerIneligible;
+        const size_t bytes = 16 + 2 * (size_t)nb * sizeof(uint64_t);
+        e = hipMalloc(&h->eager_gran, bytes);
+        if (e != hipSuccess) { h->eager_gran = nullptr; return hip_fail(h, e, "hipMalloc (eager granules)"); }
+        e = gsm::launch_granule_init(h->eager_gran, bytes, 0u, nullptr);
+        if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+        if (e == hipSuccess && !h->roll_status) {
+            e = hipMalloc(&h->roll_status, 16);
+            if (e == hipSuccess) e = clear_status(h);
+            if (e != hipSuccess) h->roll_status = nullptr;
+        }
+        if (e != hipSuccess) return hip_fail(h, e, "eager rollout setup");
+        h->eager_roll = 1;
+    }
+    // the step's outputs: the bound (or redirected) buffers, its edges too
+    p.ro = gsm::DevParams::RollOut{p.node_feat, p.reward, p.cost, p.done, p.edge_count, p.edge_ptr, p.edge_index,
+                                   p.edge_attr, 0, 0, 0, 0, 0, 0, 0, p.edge_capacity, nullptr, nullptr, p.assign, 0};
+    p.roll = gsm::DevParams::Roll{(const char *)p.actions, 0, 1, 0, 1, 0, 0, 0, 0, 0, h->eager_gran + 2,
+                                  h->roll_status, next_launch_epoch(), 0, nullptr, nullptr, 0, 0};
+    void *args[] = {&p};
+    const hipError_t e = hipLaunchKernel(fn, dim3(nb), dim3(gsm::block_threads(p)), args, (unsigned)lds, s);
+    if (e != hipSuccess) return hip_fail(h, e, "hipLaunchKernel (one-step rollout)");
+    return GSM_OK;
+}
+
 int launch(gsm_handle *h, int mode, const void *actions, int fmt, const uint8_t *mask, int reseed,
            hipStream_t s, const gsm_outputs *out = nullptr) {
     if (!h) return fail(nullptr, GSM_EINVAL, "handle is NULL");
@@ -385,6 +442,10 @@ int launch(gsm_handle *h, int mode, const void *actions, int fmt, const uint8_t 
     p.action_fmt = fmt;
     p.env_mask = mask;
     p.reseed = reseed;
+    if (mode == GSM_MODE_STEP) {
+        const int r = launch_step_roll(h, p, s);
+        if (r != kEagerIneligible) return r;
+    }
     const hipError_t e = gsm::launch_step(p, s);
     if (e != hipSuccess) return hip_fail(h, e, "kernel launch");
     return GSM_OK;
@@ -724,8 +785,9 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         depth = 4;
         if (const char *ev = getenv("GSM_ROLL_DEPTH")) depth = atoi(ev);
         depth = std::min(std::max(depth, 2), gsm::kRaggedRollMaxDepth);
-        // the env slabs of depth + 1 steps (each env's edges at a fixed stride)
-        const size_t need = (size_t)(depth + 1) * p.B * 12 * (size_t)h->sz.max_edges_per_env;
+        // the env slabs of depth + 1 steps (each env's edges at a fixed stride:
+        // max_edges_per_env + 1 words, then as many distances)
+        const size_t need = (size_t)(depth + 1) * p.B * 8 * ((size_t)h->sz.max_edges_per_env + 1);
         if (h->slab_bytes < need) {
             // a deeper ring than before: the slabs are re-allocated, and every
             // earlier ragged rollout slot is re-pointed at them (a slab holds
@@ -1166,6 +1228,7 @@ int gsm_destroy(gsm_handle *h) {
     if (h->roll_status) (void)hipFree(h->roll_status);
     if (h->edge_scratch) (void)hipFree(h->edge_scratch);
     if (h->slab) (void)hipFree(h->slab);
+    if (h->eager_gran) (void)hipFree(h->eager_gran);
     if (h->order_copied) (void)hipEventSynchronize(h->order_copied);
     if (h->block_order) (void)hipFree(h->block_order);
     if (h->order_host) (void)hipHostFree(h->order_host);

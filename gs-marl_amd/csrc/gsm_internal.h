@@ -114,7 +114,7 @@ struct DevParams {
         uint32_t *status;
         uint32_t epoch;       // this launch's epoch (20 bits), set per launch by gsm_graph_launch
         int32_t place_force;  // test knob (GSM_ROLL_PLACE=2): register, then decide identity
-        int32_t *slab;        // ragged rollout: [depth + 1][B] slabs of [2][slab_e] int32 + [slab_e] f32
+        int32_t *slab;        // ragged rollout: [depth + 1][B] slabs of [slab_e + 1] u32 row-pair words + [slab_e + 1] f32
         const int32_t *place; // ragged rollout: [W] envs by descending cost (nullptr: env = wave index)
         int32_t place_S, pad; // SIMDs the grid fills (place_R * place_S = W)
     } roll;

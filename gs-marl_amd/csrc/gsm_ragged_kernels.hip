@@ -145,6 +145,118 @@ __device__ __forceinline__ int collider_row(const Params &p, const RShape &s, in
     return l < s.N ? l : p.N + p.T + (l - s.N);
 }
 
+// ---- the pair sweep (lane = collider row m, one pass over the env's
+// collider columns c). Every predicate of the step is a function of
+// d2 = dx*dx + dy*dy, formed here by VGPR-only integer arithmetic on its bits
+// and shifted into per-lane row words (v_alignbit: word = word << 1 | sign),
+// with no compare, ballot, lane write or SGPR operand: those all issue through
+// the CU's scalar path (~1 instruction per CU and cycle, shared by its four
+// SIMDs — tools/probe_issue.hip), which the rest of the step
+// already fills. With a = bits(|dx*dx| + |dy*dy|) (non-negative, NaN above
+// every finite threshold) and na = -a (negative iff d2 > 0):
+//   0 < d2 <= R2     sign(na & (a - (bits(R2) + 1)))
+//   0 < d2 < cut2    sign(na & (a - bits(cut2)))
+//   d2 != 0          sign(na)
+// Columns run in descending order within each 32-bit word, so column c ends at
+// bit c mod 32. Collisions (d2 < dmin2 for c != m) are the other zero columns
+// plus the candidates with d2 < dmin2 (dmin2 < cut2), counted by the walk over
+// the candidate bits, which also forms contact forces where asked for (the
+// candidates are exactly the pairs the MPE force loop sums, in ascending c).
+struct RowBits {
+    uint32_t rad[2], cand[2], nz[2];   // columns [32w, 32w + 32) of word w
+};
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t shift_in_sign(uint32_t word, uint32_t x) {
+    return __builtin_amdgcn_alignbit(word, x, 31);   // (word << 1) | (x >> 31)
+}
+// pm: the lane's own position; agent columns c < N at s_pos[c], obstacle
+// columns c >= N at s_pos[orow + c] (the storage rows, orow = N_max + T_max - N)
+template <typename Params>
+__device__ __forceinline__ RowBits ragged_sweep(const Params &p, const float2 *s_pos, float2 pm, int N, int M,
+                                                int orow) {
+    // thresholds held in VGPRs (opaque to the compiler): a VALU operand in an
+    // SGPR would put every column's instruction on the scalar path
+    uint32_t r2b1 = __float_as_uint(p.R2) + 1u, cut_aa = __float_as_uint(p.cut2_aa),
+             cut_ao = __float_as_uint(p.cut2_ao);
+    asm volatile("" : "+v"(r2b1), "+v"(cut_aa), "+v"(cut_ao));
+    int zv = 0;                                   // a VGPR zero: column indices kept per lane
+    asm volatile("" : "+v"(zv));
+    const f32x2 P = {pm.x, pm.y};
+    RowBits rb = {{0u, 0u}, {0u, 0u}, {0u, 0u}};
+    auto column = [&](float2 q, uint32_t cutb, int w) {
+        const f32x2 d = P - (f32x2){q.x, q.y};
+        const f32x2 sq = d * d;
+        const uint32_t a = __float_as_uint(__builtin_fabsf(sq.x) + __builtin_fabsf(sq.y));
+        const uint32_t na = 0u - a;
+        rb.rad[w] = shift_in_sign(rb.rad[w], na & (a - r2b1));
+        rb.cand[w] = shift_in_sign(rb.cand[w], na & (a - cutb));
+        rb.nz[w] = shift_in_sign(rb.nz[w], na);
+    };
+    // columns [lo, hi) of one class from row base + c, descending
+    auto range = [&](int lo, int hi, int base, uint32_t cutb, int w) {
+        int r = base + hi - 1 + zv;
+        int c = hi - 1;
+        for (; c - 1 >= lo; c -= 2, r -= 2) {
+            const float2 q1 = s_pos[r], q0 = s_pos[r - 1];
+            column(q1, cutb, w);
+            column(q0, cutb, w);
+        }
+        if (c >= lo) column(s_pos[r], cutb, w);
+    };
+    if (M > 32) {
+        const int mid = min(max(N, 32), M);
+        range(mid, M, orow, cut_ao, 1);
+        range(32, mid, 0, cut_aa, 1);
+    }
+    const int hi0 = min(M, 32), mid0 = min(N, hi0);
+    range(mid0, hi0, orow, cut_ao, 0);
+    range(0, mid0, 0, cut_aa, 0);
+    return rb;
+}
+// The sweep's per-lane results for lane (row) m: the radius row mask, the
+// collision count (agent rows), contact candidates' forces added to *F when
+// kForce, and whether the row has another collider at d2 = 0 in an agent
+// column (App. A S16)
+template <bool kForce, typename Params>
+__device__ __forceinline__ uint64_t ragged_rows(const Params &p, const float2 *s_pos, float2 pm, int N, int M,
+                                                int orow, int lane, int *cnt, bool *zero_agent, float2 *F) {
+    const RowBits rb = ragged_sweep(p, s_pos, pm, N, M, orow);
+    const uint64_t colmask = M >= 64 ? ~0ull : ((1ull << M) - 1ull);
+    const uint64_t self = 1ull << (lane & 63);
+    const uint64_t rad = ((uint64_t)rb.rad[1] << 32 | rb.rad[0]) & colmask;
+    const uint64_t zero = ~((uint64_t)rb.nz[1] << 32 | rb.nz[0]) & colmask & ~self;
+    const uint64_t amask = N >= 64 ? ~0ull : ((1ull << N) - 1ull);
+    *zero_agent = lane < M && (zero & amask) != 0;
+    int n = 0;
+    if (lane < N) {
+        n = __popcll(zero);
+        uint64_t cm = ((uint64_t)rb.cand[1] << 32 | rb.cand[0]) & colmask;
+        float Fx = 0.0f, Fy = 0.0f;
+        if constexpr (kForce) {
+            Fx = F->x;
+            Fy = F->y;
+        }
+        const float dmin2_aa = p.dmin2_aa, dmin2_ao = p.dmin2_ao, dmin_aa = p.dmin_aa, dmin_ao = p.dmin_ao;
+        while (cm) {
+            const int c = __builtin_ctzll(cm);
+            cm &= cm - 1;
+            const bool ag = c < N;
+            const float2 q = s_pos[ag ? c : orow + c];
+            const float dx = pm.x - q.x, dy = pm.y - q.y;
+            const float d2 = dx * dx + dy * dy;
+            n += d2 < (ag ? dmin2_aa : dmin2_ao) ? 1 : 0;
+            if constexpr (kForce) {
+                const float f = contact_scale(p, d2, ag ? dmin_aa : dmin_ao);
+                Fx += f * dx;
+                Fy += f * dy;
+            }
+        }
+        if constexpr (kForce) *F = make_float2(Fx, Fy);
+    }
+    *cnt = n;
+    return lane < M ? rad : 0ull;
+}
+
 // slot j (< N) of a polygon/line env from its target positions (lanes 0/1)
 template <typename Params>
 __device__ __forceinline__ float2 slot_of(const Params &p, const RShape &s, int lane, float2 tp) {
@@ -605,26 +717,29 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
     }
     stage();
 
+    // the env's colliders and targets at their storage rows of s_pos (the
+    // column loops of the pair sweep read them)
+    const int orow = Nmax + Tmax;   // obstacle column c at s_pos[orow - N + c]
+    auto stage_rows = [&]() {
+        if (lane < s.M) s_pos[collider_row(p, s, lane)] = cp;
+        if (lane < s.T) s_pos[Nmax + lane] = tp;
+        wave_sync();
+    };
     bool done = false;
     if (p.mode == kModeStep) {
-        // _set_action + apply_environment_force + integrate_state (App. A S3-S6)
-        float Fx = 0.0f, Fy = 0.0f;
-        if (lane < s.N) {
-            const float2 u = action_force(p, eb * Nmax + lane);
-            Fx = u.x;
-            Fy = u.y;
+        // _set_action + apply_environment_force + integrate_state (App. A S3-S6):
+        // the action force, then the contacts of the candidate pairs in
+        // ascending collider order (ragged_rows)
+        float2 F = make_float2(0.0f, 0.0f);
+        if (lane < s.N) F = action_force(p, eb * Nmax + lane);
+        stage_rows();
+        {
+            int unused_n;
+            bool unused_z;
+            (void)ragged_rows<true>(p, s_pos, cp, s.N, s.M, orow - s.N, lane, &unused_n, &unused_z, &F);
         }
-        for (int c = 0; c < s.M; ++c) {
-            const float2 q = rl_f2(cp, c);
-            const float dx = cp.x - q.x, dy = cp.y - q.y;
-            const float d2 = dx * dx + dy * dy;
-            const bool ag = c < s.N;
-            if (lane < s.N && c != lane && d2 > 0.0f && d2 < (ag ? p.cut2_aa : p.cut2_ao)) {
-                const float f = contact_scale(p, d2, ag ? p.dmin_aa : p.dmin_ao);
-                Fx += f * dx;
-                Fy += f * dy;
-            }
-        }
+        wave_sync();   // s_pos is re-staged after the integration
+        float Fx = F.x, Fy = F.y;
         if (p.strict) {   // App. A S16 strict: MPE's 0/0 force (every lane runs the readlanes)
             const bool bad = strict_bad(lane, cp, s.N, s.M, [&](int c) { return rl_f2(cp, c); });
             if (lane < s.N && bad) {
@@ -656,21 +771,11 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
     // on either side, App. A S16)
     bool coinc = false;
     auto pair_sweep = [&](int *cnt) {
-        uint64_t rm = 0;
-        int n = 0;
-        bool z = false;
-        for (int c = 0; c < s.M; ++c) {
-            const float2 q = rl_f2(cp, c);
-            const float dx = cp.x - q.x, dy = cp.y - q.y;
-            const float d2 = dx * dx + dy * dy;
-            const bool other = c != lane;
-            n += (other && d2 < (c < s.N ? p.dmin2_aa : p.dmin2_ao)) ? 1 : 0;
-            rm |= (other && d2 > 0.0f && d2 <= p.R2) ? (1ull << c) : 0ull;
-            z |= other && d2 == 0.0f && c < s.N;
-        }
-        *cnt = n;
-        coinc = __any(lane < s.M && z);
-        return lane < s.M ? rm : 0ull;
+        stage_rows();
+        bool z;
+        const uint64_t rm = ragged_rows<false>(p, s_pos, cp, s.N, s.M, orow - s.N, lane, cnt, &z, nullptr);
+        coinc = __any(z);
+        return rm;
     };
     int cnt = 0;
     uint64_t rmask = pair_sweep(&cnt);
@@ -1040,6 +1145,78 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_ragged_kernel(DevParams p) {
     ragged_env_emit(p, b, lane, off, smem + wave * p.wave_lds_emit, EdgeSink{p.edge_index, p.edge_attr, p.edge_capacity});
 }
 
+// ---- the ragged rollout's compact edge lists. A step's edges are first
+// expanded, in CSR order, into (source row | destination row << 8) words — rows
+// of the env's storage layout — by every lane walking the set bits of its own
+// row mask: per bit a v_ffbl, the word and an LDS or HBM write at the row's
+// next offset; a lane whose row is exhausted writes a spare word instead (the
+// address picked by a bit mask, no compare), so the walk runs the wave's
+// longest row with no per-lane branch. Written out (and packed `depth` steps
+// later) by all 64 lanes, edge e by lane e mod 64.
+__device__ __forceinline__ int ffbl_or_neg(uint32_t x) {   // lowest set bit, -1 for 0
+    int r;
+    asm("v_ffbl_b32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+__device__ __forceinline__ int wave_max(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x111, 0xf, 0xf, false));   // row_shr:1
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x112, 0xf, 0xf, false));   // row_shr:2
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x114, 0xf, 0xf, false));   // row_shr:4
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x118, 0xf, 0xf, false));   // row_shr:8
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xa, 0xf, false));   // row_bcast:15
+    v = max(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xc, 0xf, false));   // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+// The env's edges of one step in CSR order (agent rows: agent columns, the
+// agent's target edges, obstacle columns; target rows; obstacle rows: agent
+// then obstacle columns), each through put(at, src_row, dst_row) with
+// at < total, or at = spare for a lane with nothing to write. Returns total.
+template <typename Params, typename Put>
+__device__ __forceinline__ int ragged_expand(const Params &p, const RShape &s, int lane, uint64_t mask,
+                                             uint32_t spare, Put &&put) {
+    const int Nmax = p.N, orow = p.N + p.T - s.N;
+    const uint32_t abits = s.N >= 32 ? ~0u : ((1u << s.N) - 1u);
+    const uint32_t am = (uint32_t)mask & abits, om0 = (uint32_t)mask & ~abits, om1 = (uint32_t)(mask >> 32);
+    const bool agent = lane < s.N;
+    const int na = __popc(am), no0 = __popc(om0), no1 = __popc(om1);
+    const int cnt = na + no0 + no1 + (agent ? s.Tper : 0);
+    const int incl = wave_scan(cnt);
+    const int agent_total = s.N > 0 ? __builtin_amdgcn_readlane(incl, s.N - 1) : 0;
+    const int total = __builtin_amdgcn_readlane(incl, kWave - 1) + s.N * s.Tper;
+    uint32_t o = (uint32_t)(incl - cnt + (agent ? 0 : s.N * s.Tper));
+    const uint32_t src = (uint32_t)(agent ? lane : orow + lane);
+    auto walk = [&](uint32_t wd, int n_it, uint32_t rowbase) {
+        for (int i = 0; i < n_it; ++i) {
+            const int c = ffbl_or_neg(wd);
+            const uint32_t none = (uint32_t)(c >> 31);   // all ones once the row is exhausted
+            wd &= wd - 1u;
+            put((none & spare) | (~none & o), src, rowbase + (uint32_t)c);
+            o += 1u + none;
+        }
+    };
+    walk(am, wave_max(na), 0u);
+    if (agent) {   // the agent's own target edges, between its agent and obstacle columns
+        if (s.scn == kScnNav) {
+            put(o++, src, (uint32_t)(Nmax + lane));
+        } else {
+            put(o++, src, (uint32_t)Nmax);
+            if (s.Tper == 2) put(o++, src, (uint32_t)(Nmax + 1));
+        }
+    }
+    walk(om0, wave_max(no0), (uint32_t)orow);
+    walk(om1, wave_max(no1), (uint32_t)(orow + 32));
+    if (agent) {   // target rows: goal i -> agent i; centre / line ends -> every agent
+        const uint32_t tb = (uint32_t)agent_total;
+        if (s.scn == kScnNav) {
+            put(tb + lane, (uint32_t)(Nmax + lane), (uint32_t)lane);
+        } else {
+            put(tb + lane, (uint32_t)Nmax, (uint32_t)lane);
+            if (s.Tper == 2) put(tb + s.N + lane, (uint32_t)(Nmax + 1), (uint32_t)lane);
+        }
+    }
+    return total;
+}
+
 // ---------------------------------------------------------------------------
 // Fused rollout of a ragged batch (GSM_GRAPH_ROLL; config C4)
 // ---------------------------------------------------------------------------
@@ -1306,13 +1483,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     // launch parameters read at the point of use (late_params): held across
     // the loop they would not fit the 78-SGPR / 64-VGPR budget
     auto P = [&]() -> KernargParams & { return late_params(); };
-    // the env's edge slab at ring position j (step mod depth + 1): [2][slab_e]
-    // int32 node ids, [slab_e] f32
-    auto slab_of = [&](const int j) -> EdgeSink {
+    // the env's edge slab at ring position j (step mod depth + 1): slab_e + 1
+    // (source row | destination row << 8) words (the last one a spare), then
+    // as many f32 distances
+    struct Slab {
+        uint32_t *word;
+        float *attr;
+    };
+    auto slab_of = [&](const int j) -> Slab {
         KernargParams &q = late_params();
-        const int64_t per = 3 * (int64_t)q.roll.slab_e;
+        const int64_t per = 2 * ((int64_t)q.roll.slab_e + 1);
         int32_t *base = q.roll.slab + ((int64_t)j * q.B + eb) * per;
-        return EdgeSink{base, (float *)(base + 2 * q.roll.slab_e), q.roll.slab_e};
+        return Slab{(uint32_t *)base, (float *)(base + q.roll.slab_e + 1)};
     };
     int ring = 0;                    // k mod (depth + 1): the slab / count of the current step
     const bool glast = (w & 63) == 63;
@@ -1331,43 +1513,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     // would spill.
     // radius row masks and collision counts (as ragged_env_step) and, with
     // `nxt`, the forces of the step whose actions are in row `row`
+    // (the env's colliders and targets staged at their storage rows of s_pos:
+    // the sweep's column loops and the emission read them)
     auto pair_sweep = [&](int *cnt, const bool nxt, const int row) {
-        uint64_t rm = 0;
-        int n = 0;
-        bool z = false;
-        float Fx = 0.0f, Fy = 0.0f;
-        if (nxt && lane < s.N) {
-            const float2 u = roll_action_force(late_params(), row, eb * Nmax + lane);
-            Fx = u.x;
-            Fy = u.y;
-        }
-        for (int c = 0; c < s.M; ++c) {
-            const float2 q = rl_f2(cp, c);
-            const float dx = cp.x - q.x, dy = cp.y - q.y;
-            const float d2 = dx * dx + dy * dy;
-            const bool other = c != lane, ag = c < s.N;
-            n += (other && d2 < (ag ? P().dmin2_aa : P().dmin2_ao)) ? 1 : 0;
-            rm |= (other && d2 > 0.0f && d2 <= P().R2) ? (1ull << c) : 0ull;
-            z |= other && d2 == 0.0f && ag;
-            if (nxt && lane < s.N && other && d2 > 0.0f && d2 < (ag ? P().cut2_aa : P().cut2_ao)) {
-                const float f = contact_scale(P(), d2, ag ? P().dmin_aa : P().dmin_ao);
-                Fx += f * dx;
-                Fy += f * dy;
-            }
-        }
+        if (lane < s.M) s_pos[collider_row(P(), s, lane)] = cp;
+        if (lane < s.T) s_pos[Nmax + lane] = tp;
+        wave_sync();
+        float2 F = make_float2(0.0f, 0.0f);
+        if (nxt && lane < s.N) F = roll_action_force(late_params(), row, eb * Nmax + lane);
+        bool z;
+        const uint64_t rm = ragged_rows<true>(P(), s_pos, cp, s.N, s.M, Nmax + Tmax - s.N, lane, cnt, &z, &F);
         if (nxt && P().strict) {
             const bool bad = strict_bad(lane, cp, s.N, s.M, [&](int c) { return rl_f2(cp, c); });
-            if (lane < s.N && bad) {
-                Fx = __builtin_nanf("");
-                Fy = __builtin_nanf("");
-            }
+            if (lane < s.N && bad) F = make_float2(__builtin_nanf(""), __builtin_nanf(""));
         }
-        if (nxt && lane < kRaggedMaxAgents) s_fn[lane] = make_float2(Fx, Fy);
-        *cnt = n;
-        coinc = __any(lane < s.M && z);
-        return lane < s.M ? rm : 0ull;
+        if (nxt && lane < kRaggedMaxAgents) s_fn[lane] = F;
+        coinc = __any(z);
+        return rm;
     };
     // step k's edge count published, its edges written to the env's slab
+    // (from the positions the sweep staged)
     auto publish = [&](const int k) {   // at ring position `ring`
         const int edges = wave_sum((int)__popcll(rmask)) + 2 * s.N * s.Tper;
         if (lane == 0) {
@@ -1375,10 +1540,33 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             xfer_st(x.agg + (int64_t)k * x.W + w, x.tag(k), (uint32_t)edges);
             s_cnt[ring] = edges;
         }
-        if (lane < s.M) s_pos[collider_row(P(), s, lane)] = cp;
-        if (lane < s.T) s_pos[Nmax + lane] = tp;
-        wave_sync();
-        if (live) ragged_env_emit_rows(P(), w, lane, 0, s_pos, s, rmask, slab_of(ring));
+        if (live) {
+            const Slab sl = slab_of(ring);
+            // the assignment's LDS is free here (before this step's assignment,
+            // or after the reset's): the list is expanded there when it fits
+            uint32_t *const scr = (uint32_t *)lds;
+            const int cap = lsa_lds_bytes(Nmax) / 4 - 1;   // the last word is the spare
+            if (edges <= cap) {
+                (void)ragged_expand(P(), s, lane, rmask, (uint32_t)cap,
+                                    [&](uint32_t at, uint32_t a, uint32_t b) { scr[at] = a | b << 8; });
+                wave_sync();
+                for (int e = lane; e < edges; e += kWave) {
+                    const uint32_t wd = scr[e];
+                    const float2 pa = s_pos[wd & 0xffu], pb = s_pos[wd >> 8];
+                    const float dx = pa.x - pb.x, dy = pa.y - pb.y;
+                    sl.word[e] = wd;
+                    sl.attr[e] = sqrtf(dx * dx + dy * dy);
+                }
+            } else {   // straight into the slab (its spare word at slab_e)
+                const uint32_t spare = (uint32_t)P().roll.slab_e;
+                (void)ragged_expand(P(), s, lane, rmask, spare, [&](uint32_t at, uint32_t a, uint32_t b) {
+                    const float2 pa = s_pos[a], pb = s_pos[b];
+                    const float dx = pa.x - pb.x, dy = pa.y - pb.y;
+                    sl.word[at] = a | b << 8;
+                    sl.attr[at] = sqrtf(dx * dx + dy * dy);
+                });
+            }
+        }
         wave_sync();
         cur_edges = edges;
     };
@@ -1398,11 +1586,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             eptr[w] = off;
             if (w == q.B - 1) eptr[q.B] = off + cnt;
         }
-        const EdgeSink src = slab_of(jr), dst = roll_edge_sink<kSlots>(q, j, K);
+        const Slab src = slab_of(jr);
+        const EdgeSink dst = roll_edge_sink<kSlots>(q, j, K);
+        int32_t g0 = (int32_t)(eb * Emax);   // the env's first global node id
+        asm volatile("" : "+v"(g0));
         for (int e = lane; e < cnt; e += kWave) {
             if (off + e < dst.cap) {   // a redirected slot may be smaller than the worst case
-                dst.index[off + e] = src.index[e];
-                dst.index[dst.cap + off + e] = src.index[src.cap + e];
+                const uint32_t wd = src.word[e];
+                dst.index[off + e] = g0 + (int32_t)(wd & 0xffu);
+                dst.index[dst.cap + off + e] = g0 + (int32_t)(wd >> 8);
                 dst.attr[off + e] = src.attr[e];
             }
         }

@@ -74,6 +74,10 @@ def main(path, kname):
                 loop_of[cur] = (".LBB" + h.group(1), int(h.group(2)))
             continue
         t = l.strip()
+        if t.startswith(";") and "Loop Header" in t and blocks[cur].total() == 0:
+            # the loop annotation on the line after the label ("Parent Loop ...")
+            loop_of[cur] = (cur, int(re.search(r"Depth=(\d+)", t).group(1)))
+            continue
         if not t or t.startswith((";", ".", "//")):
             continue
         parts = t.split(None, 1)
