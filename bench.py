@@ -376,6 +376,9 @@ def parse_args(argv=None):
     ap.add_argument("--policy", action="store_true",
                     help="closed loop: GpuGraphVecEnv(output='torch', graph='coo').step() with an on-device "
                          "greedy policy reading each step's obs (the runner's path; context, not the headline)")
+    ap.add_argument("--policy-graph", action="store_true",
+                    help="the closed loop of --policy with the policy and env.step captured into one "
+                         "torch.cuda graph per step (replayed every step)")
     ap.add_argument("--unfused", action="store_true",
                     help="two launches per step in the graphs (no lagged emission)")
     ap.add_argument("--no-roll", action="store_true",
@@ -507,6 +510,8 @@ def run_rank(args):
     N, B = spec["n_agents"], spec["n_envs"]
     cfg = shard_config(EnvConfig(seed=1234, **spec), rank, world)
     venv = None
+    if args.policy_graph:
+        args.policy = True
     if args.policy and not stub:
         # the vec-env a GS-MARL runner drives (gsmarl_amd/vec_env.py), on device
         from gsmarl_amd.vec_env import GpuGraphVecEnv
@@ -586,9 +591,26 @@ def run_rank(args):
         return torch.where(dx.abs() > dy.abs(), torch.where(dx > 0, 1, 2),
                            torch.where(dy > 0, 3, 4)).to(torch.int32)
 
+    pgraph = None
+    if args.policy_graph and not stub:
+        # policy + env.step of one step as one torch CUDA graph (gsm_step on a
+        # capturing stream takes the two-launch path: no per-launch state)
+        side = torch.cuda.Stream(device=dev)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):   # warm the allocator and the policy's kernels (untimed steps)
+                venv.step(greedy(obs))
+        torch.cuda.current_stream().wait_stream(side)
+        pgraph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(pgraph):
+            venv.step(greedy(obs))   # obs: a view of the env's node features, static
+
     def run_steps(n, slot):
         nonlocal obs
-        if venv is not None:
+        if pgraph is not None:
+            for t in range(n):
+                pgraph.replay()
+        elif venv is not None:
             for t in range(n):
                 obs = venv.step(greedy(obs))[0]
         elif args.eager:
@@ -722,7 +744,10 @@ def run_rank(args):
                        "agents_per_step": agents,
                        "episode_length": EL, "mean_edges_per_env": round(total_edges / B, 2),
                        "parallelism": f"env-sharded x{world} (no data-path collective)",
-                       "launch": ("closed loop: GpuGraphVecEnv(output='torch', graph='coo').step(policy(obs)) "
+                       "launch": ("closed loop, one torch.cuda graph per step: greedy on-device policy(obs) + "
+                                  "GpuGraphVecEnv(output='torch', graph='coo').step (step + emit kernels)"
+                                  if pgraph is not None else
+                                  "closed loop: GpuGraphVecEnv(output='torch', graph='coo').step(policy(obs)) "
                                   "per step, greedy on-device policy" if venv is not None else
                                   "eager" if args.eager else ("rollout buffer (GraphRolloutBuffer.capture): "
                                   f"one launch per {EL}-step episode, step k's outputs into slot k+1 "

@@ -388,6 +388,11 @@ hipError_t clear_status(gsm_handle *h);
 constexpr int kEagerIneligible = 1;
 int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
     if (h->eager_roll == 0 || p.path == gsm::kPathRagged) return kEagerIneligible;
+    // a stream being captured into a graph (e.g. torch.cuda.graph around a
+    // policy + env.step): the two launches, which hold no per-launch state —
+    // a captured rollout launch would replay one launch epoch every time
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return kEagerIneligible;
     const bool tile = p.path == gsm::kPathTile;
     const void *fn = tile ? gsm::roll_tile_kernel_fn(p, false) : gsm::roll_seg_kernel_fn(p, false);
     if (!fn) return kEagerIneligible;   // (the action format may differ per call: checked every time)

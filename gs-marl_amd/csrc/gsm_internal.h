@@ -15,8 +15,10 @@ constexpr int kTileEmitScr = 6144;   // tile emitter: staged edge words per env 
 constexpr int kRaggedMaxAgents = 32;                                  // = GSM_RAGGED_MAX_AGENTS
 constexpr int kRaggedTable = kRaggedMaxAgents * (kRaggedMaxAgents + 1) / 2;   // rows n = 1..32
 // ragged assignment scratch per wave (gsm_ragged_kernels.hip LsaLds): cost
-// matrix rows (a multiple of 8) at an odd stride, column and row duals, column -> row
-__host__ __device__ constexpr int lsa_stride(int nmax) { return nmax | 1; }
+// matrix rows (a multiple of 8) at an odd stride of at least that many
+// columns (the row passes read whole chunks of 8: the columns past N hold
+// +inf), column and row duals, column -> row
+__host__ __device__ constexpr int lsa_stride(int nmax) { return ((nmax + 7) & ~7) | 1; }
 __host__ __device__ constexpr int lsa_cost_bytes(int nmax) { return 4 * ((nmax + 7) & ~7) * lsa_stride(nmax); }
 __host__ __device__ constexpr int lsa_lds_bytes(int nmax) {
     return ((lsa_cost_bytes(nmax) + 15) & ~15) + 16 * kRaggedMaxAgents + 4 * kRaggedMaxAgents;

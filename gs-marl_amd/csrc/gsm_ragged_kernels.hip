@@ -333,9 +333,11 @@ __device__ __forceinline__ LsaLds lsa_lds(unsigned char *lds, int nmax) {
 // kColLds: the path loop reads C[i][lane] from the LDS copy instead of a
 // 32-register column (the rollout kernel's 64-VGPR budget; one LDS read on the
 // loop's chain, same values: identical results).
+// s_agent: the agents' positions in LDS (rows 0..N-1: the staged storage
+// rows), read as broadcasts when the cost matrix is built
 template <bool kColLds = false>
-__device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &sl, float *own, LsaWarm w,
-                        int *iters = nullptr, uint64_t *tm = nullptr) {
+__device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const float2 *s_agent, const LsaLds &sl, float *own,
+                        LsaWarm w, int *iters = nullptr, uint64_t *tm = nullptr) {
     const bool col = lane < N;
     float *const s_cost = sl.cost;
     const int S = sl.S;
@@ -351,21 +353,25 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
     // the LDS copy serves the row-parallel passes and the final cost lookup.
     // Rows in groups of 8 with no per-row branch, so the (correctly rounded)
     // square roots of a group are independent instructions; rows >= N of the
-    // last group are computed and never read.
+    // last group are computed and never read by the path loop (the column
+    // pass gives them u = -inf). Columns N..roundup8(N)-1 of every row hold
+    // +inf, so the row passes run whole chunks of 8 with no per-column test.
     float ccol[kColLds ? 1 : kRaggedMaxAgents];
+    const int n8 = (N + 7) & ~7;
+    const bool pad = !col && lane < n8;
 #pragma unroll
     for (int i0 = 0; i0 < kRaggedMaxAgents; i0 += 8) {
         if (i0 < N) {
             float c8[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                const float2 pi = rl_f2(pa, i0 + k);
+                const float2 pi = s_agent[i0 + k];
                 const float dx = pi.x - slot.x, dy = pi.y - slot.y;
                 c8[k] = sqrtf(dx * dx + dy * dy);
             }
 #pragma unroll
             for (int k = 0; k < 8; ++k) {
-                if (col) s_cost[(i0 + k) * S + lane] = c8[k];
+                if (col || pad) s_cost[(i0 + k) * S + lane] = col ? c8[k] : __builtin_inff();
                 if constexpr (!kColLds) ccol[i0 + k] = c8[k];
             }
         } else if constexpr (!kColLds) {
@@ -503,20 +509,40 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
     // from row i to the row holding column j for every tight unmatched (i, j)
     // is acyclic (peeled sink by sink)
     auto certified = [&](double tau = 1e-9) -> bool {
-        // row-parallel: lane i checks row i against the column duals in LDS
-        if (lane < kRaggedMaxAgents) sl.v[lane] = v;
+        // row-parallel: lane i checks row i against the column duals in LDS,
+        // by VGPR arithmetic only (no per-column compare or select): the
+        // smallest reduced cost over all columns (>= -1e-11 together with
+        // |r| <= 1e-11 on the matched column is the same test as per column),
+        // and the tight bits r <= tau as the sign of r - succ(tau), shifted in
+        // (columns past N hold +inf: never tight)
+        if (lane < kRaggedMaxAgents) sl.v[lane] = col ? v : 0.0;
         wave_sync();
         bool good = true;
         uint32_t tight = 0;   // lane i: tight unmatched columns of row i
         if (col) {
             const float *crow = s_cost + lane * S;
             const int ci = col4row;
-#pragma unroll 4
-            for (int j = 0; j < N; ++j) {
-                const double r = (double)crow[j] - u - sl.v[j];
-                good &= j == ci ? fabs(r) <= 1e-11 : r >= -1e-11;
-                tight |= (j != ci && r <= tau) ? 1u << j : 0u;
+            const double tau1 = __longlong_as_double(__double_as_longlong(tau) + 1);   // succ(tau), tau > 0
+            double rmin = kInf;
+            for (int j0 = n8 - 4; j0 >= 0; j0 -= 4) {   // descending: column j ends at bit j
+                float cr[4];
+                double vj[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    cr[k] = crow[j0 + k];
+                    vj[k] = sl.v[j0 + k];
+                }
+#pragma unroll
+                for (int k = 3; k >= 0; --k) {
+                    const double r = (double)cr[k] - u - vj[k];
+                    rmin = fmin(rmin, r);
+                    const uint32_t hi = (uint32_t)((uint64_t)__double_as_longlong(r - tau1) >> 32);
+                    tight = __builtin_amdgcn_alignbit(tight, hi, 31);
+                }
             }
+            const double rc = ci >= 0 ? (double)crow[ci] - u - sl.v[ci] : 0.0;
+            good = rmin >= -1e-11 && fabs(rc) <= 1e-11;
+            if (ci >= 0) tight &= ~(1u << ci);
         }
         if (!__all(good)) {
 #ifdef GSM_STAMPS   // diagnostic builds: why the certificate failed (bits 24+)
@@ -565,8 +591,10 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
                     const float *crow = s_cost + lane * S;
                     // chunks of 8 columns: every LDS read of a chunk is issued
                     // before the first use (one wait per chunk); columns past
-                    // N read scratch and are masked
-                    for (int j0 = 0; j0 < N; j0 += 8) {
+                    // N hold +inf (and v = 0): r = +inf, no per-column test
+                    // (the minimum by v_min_f64: no zero of either sign
+                    // arises, C - v is +0 when equal, and no NaN)
+                    for (int j0 = 0; j0 < n8; j0 += 8) {
                         float cr[8];
                         double vj[8];
 #pragma unroll
@@ -575,10 +603,7 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
                             vj[k] = sl.v[j0 + k];
                         }
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) {
-                            const double r = (double)cr[k] - vj[k];
-                            m = (j0 + k < N && r < m) ? r : m;
-                        }
+                        for (int k = 0; k < 8; ++k) m = fmin(m, (double)cr[k] - vj[k]);
                     }
                     // the previous column's reduced cost, the same expression as in the scan
                     rc = (c0 >= 0 && c0 < N) ? (double)crow[c0] - sl.v[c0] : kInf;
@@ -591,11 +616,12 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
             // row minima again. Fewer rows lose their previous column: 12.2 ->
             // 8.9 of 24 in a polygon simulation (oracle/lsa_ref.py duals,
             // random actions); further rounds keep 8.9.
-            if (lane < kRaggedMaxAgents) sl.u[lane] = col ? m : 0.0;
+            // (rows past N get u = -inf: r = +inf, no per-row test)
+            if (lane < kRaggedMaxAgents) sl.u[lane] = col ? m : -kInf;
             wave_sync();
             if (col) {
                 double cm = kInf;
-                for (int i0 = 0; i0 < N; i0 += 8) {   // chunks of 8 rows, reads first
+                for (int i0 = 0; i0 < n8; i0 += 8) {   // chunks of 8 rows, reads first
                     float cc[8];
                     double ui[8];
 #pragma unroll
@@ -604,10 +630,7 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const LsaLds &s
                         ui[k] = sl.u[i0 + k];
                     }
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const double r = (double)cc[k] - ui[k];
-                        cm = (i0 + k < N && r < cm) ? r : cm;
-                    }
+                    for (int k = 0; k < 8; ++k) cm = fmin(cm, (double)cc[k] - ui[k]);
                 }
                 v = cm;
             }
@@ -796,9 +819,9 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
         int nit = 0;
         GSM_STAMP(p, b, 0);
 #ifdef GSM_STAMPS
-        sigma = wave_lsa(s.N, lane, cp, slot, s_lsa, &own, lsa_warm, &nit, p.stamps ? p.stamps + (int64_t)b * 16 + 4 : nullptr);
+        sigma = wave_lsa(s.N, lane, cp, slot, s_pos, s_lsa, &own, lsa_warm, &nit, p.stamps ? p.stamps + (int64_t)b * 16 + 4 : nullptr);
 #else
-        sigma = wave_lsa(s.N, lane, cp, slot, s_lsa, &own, lsa_warm, &nit);
+        sigma = wave_lsa(s.N, lane, cp, slot, s_pos, s_lsa, &own, lsa_warm, &nit);
 #endif
         GSM_STAMP(p, b, 1);
 #ifdef GSM_STAMPS
@@ -831,7 +854,7 @@ __device__ int ragged_env_step(const DevParams &p, const int b, const int lane, 
             if (s.scn != kScnNav) {
                 slot = slot_of(p, s, lane, tp);
                 float own;
-                sigma = wave_lsa(s.N, lane, cp, slot, s_lsa, &own, lsa_warm);
+                sigma = wave_lsa(s.N, lane, cp, slot, s_pos, s_lsa, &own, lsa_warm);
             }
         }
     }
@@ -1661,7 +1684,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             // them hold zeros)
             if (lane < kRaggedMaxAgents) s_stash[lane] = make_float4(v.x, v.y, tp.x, tp.y);
             s_rm[lane] = rmask;
-            sigma = wave_lsa<true>(s.N, lane, cp, slot, s_lsa, &own, lw);
+            sigma = wave_lsa<true>(s.N, lane, cp, slot, s_pos, s_lsa, &own, lw);
             const float4 st = lane < kRaggedMaxAgents ? s_stash[lane] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             v = make_float2(st.x, st.y);
             tp = make_float2(st.z, st.w);

@@ -195,11 +195,18 @@ __device__ __forceinline__ uint64_t agent_bits_of_word(int N, int k) {   // agen
 // words are read (keep_oo) — the same buffer except in the fused rollout,
 // which double-buffers the masks in LDS (the previous step's are emitted
 // later); cout: where the contact words go (LDS in the rollout)
+// kN > 0: a compiled shape (kN agents, kNo obstacles), else the config's
+#define GSM_TILE_SHAPE(p)                                                 \
+    const int N = kN > 0 ? kN : (p).N, No = kN > 0 ? kNo : (p).No;        \
+    const int M = N + No, E = 2 * N + No;                                 \
+    const int W = kN > 0 ? (kN + kNo + 63) / 64 : (p).W;                  \
+    (void)M, (void)E, (void)W, (void)No
+template <int kN = 0, int kNo = 0>
 __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s_pos, const TileSymLds &S,
                                              int *s_cost, int64_t eb, bool keep_oo, uint64_t *rout = nullptr,
                                              const uint64_t *rkeep = nullptr, uint64_t *cout = nullptr) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
-    const int N = p.N, M = p.M, W = p.W, No = p.No;
+    GSM_TILE_SHAPE(p);
     const int tid = threadIdx.x, lane = tid & 63;
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int NB8 = (N + 7) >> 3, NP = (N + 1) >> 1;
@@ -264,6 +271,7 @@ __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s
         if (r < N) {
             const uint64_t *ar = S.arow + (int64_t)r * 2 * W;
             int cnt = 0;
+#pragma unroll 1
             for (int k = 0; k < W; ++k) {
                 const uint64_t self = k == (r >> 6) ? 1ull << (r & 63) : 0ull;
                 const uint64_t rad = ar[k] & ~self;
@@ -288,6 +296,7 @@ __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s
             s_cost[r] = cnt;
         } else {
             const uint64_t *ow = S.own + (int64_t)(r - N) * W;
+#pragma unroll 1
             for (int k = 0; k < W; ++k) {
                 const uint64_t am = agent_bits_of_word(N, k);
                 uint64_t oo = 0;
@@ -356,10 +365,10 @@ __device__ __forceinline__ int obs_sweep_any(const DevParams &p, const float2 *s
 // Row r's edges in entity order from its radius mask words: agent rows ->
 // agents, own goal (always), obstacles; goal rows -> own agent; obstacle rows
 // -> agents, obstacles. kWrite = false only counts.
-template <bool kWrite>
+template <bool kWrite, int kN = 0, int kNo = 0>
 __device__ __forceinline__ int row_edges(const DevParams &p, const EdgeSink &out, const float2 *s_pos,
                                          const uint64_t *rmask, int r, int64_t off, int32_t g0) {
-    const int N = p.N, W = p.W;
+    GSM_TILE_SHAPE(p);
     if (r >= N && r < 2 * N) {   // goal row: goal i -> agent i
         if (kWrite && off < out.cap) {
             const float2 a = s_pos[r], q = s_pos[r - N];
@@ -390,6 +399,7 @@ __device__ __forceinline__ int row_edges(const DevParams &p, const EdgeSink &out
         ++n;
     };
     bool goal_done = r >= N;
+#pragma unroll 1
     for (int k = 0; k < W; ++k) {
         uint64_t bits = row[k];
         while (bits) {
@@ -408,8 +418,9 @@ __device__ __forceinline__ int row_edges(const DevParams &p, const EdgeSink &out
 
 // Row r's edges in entity order as (source | destination << 16) entity-id
 // words at `at` (the staged form of row_edges<true>); returns the end.
+template <int kN = 0, int kNo = 0>
 __device__ __forceinline__ uint32_t *expand_row(const DevParams &p, const uint64_t *rmask, int r, uint32_t *at) {
-    const int N = p.N, W = p.W;
+    GSM_TILE_SHAPE(p);
     const uint32_t src = (uint32_t)r;
     if (r >= N && r < 2 * N) {   // goal row: goal i -> agent i
         *at = src | ((uint32_t)(r - N) << 16);
@@ -417,6 +428,7 @@ __device__ __forceinline__ uint32_t *expand_row(const DevParams &p, const uint64
     }
     const uint64_t *row = rmask + (int64_t)(r < N ? r : r - N) * W;
     bool goal_done = r >= N;
+#pragma unroll 1
     for (int k = 0; k < W; ++k) {
         for (uint64_t bits = row[k]; bits; bits &= bits - 1) {
             const int c = 64 * k + __builtin_ctzll(bits);
@@ -441,15 +453,16 @@ __device__ __forceinline__ uint32_t *expand_row(const DevParams &p, const uint64
 // thread, edge e by thread e mod 512 — coalesced stores and no row-length
 // imbalance; otherwise each thread writes its runs directly (bounded by the
 // output capacity). s_red: 2 * kTileWaves ints.
+template <int kN = 0, int kNo = 0>
 __device__ __forceinline__ void emit_env(const DevParams &p, const EdgeSink &out, const float2 *s_pos,
                                          const uint64_t *rmask, int before, int64_t *off_out, int *s_red,
                                          uint32_t *s_scr, int scr_cap, int32_t g0) {
     const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-    const int E = p.E;
+    GSM_TILE_SHAPE(p);
     const int R = (E + kTileBlock - 1) / kTileBlock;
     const int r0 = tid * R, r1 = min(E, r0 + R);
     int mine = 0;
-    for (int r = r0; r < r1; ++r) mine += row_edges<false>(p, out, s_pos, rmask, r, 0, g0);
+    for (int r = r0; r < r1; ++r) mine += row_edges<false, kN, kNo>(p, out, s_pos, rmask, r, 0, g0);
     const int incl = wave_scan(mine);
     const int btot = wave_total(before);
     if (lane == 63) s_red[wave] = incl;
@@ -468,7 +481,7 @@ __device__ __forceinline__ void emit_env(const DevParams &p, const EdgeSink &out
     }
     if (total <= scr_cap && off + total <= out.cap) {   // workgroup-uniform
         uint32_t *at = s_scr + base;
-        for (int r = r0; r < r1; ++r) at = expand_row(p, rmask, r, at);
+        for (int r = r0; r < r1; ++r) at = expand_row<kN, kNo>(p, rmask, r, at);
         __syncthreads();
         int32_t *src = out.index + off, *dst = out.index + out.cap + off;
         float *attr = out.attr + off;
@@ -483,7 +496,7 @@ __device__ __forceinline__ void emit_env(const DevParams &p, const EdgeSink &out
         }
     } else {
         int64_t o = off + base;
-        for (int r = r0; r < r1; ++r) o += row_edges<true>(p, out, s_pos, rmask, r, o, g0);
+        for (int r = r0; r < r1; ++r) o += row_edges<true, kN, kNo>(p, out, s_pos, rmask, r, o, g0);
     }
 }
 
@@ -767,12 +780,15 @@ size_t roll_tile_kernel_lds(const DevParams &p) {
            8 * (size_t)p.W * (2 * p.M + p.N);
 }
 
-template <bool kSlots>   // per-step outputs at base + k * stride (a rollout buffer), else in place
+// kN > 0: compiled for kN agents and kNo obstacles (C3: 96 + 96), so the
+// shape is immediates throughout the loop instead of values held in SGPRs
+// (at 8 waves per SIMD those spilled to VGPR lanes: a v_readlane at every use)
+template <bool kSlots, int kN = 0, int kNo = 0>   // kSlots: per-step outputs at base + k * stride (a rollout buffer)
 __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel(DevParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
-    const int N = p.N, E = p.E, W = p.W, M = p.M;
+    GSM_TILE_SHAPE(p);
     float2 *s_pos = (float2 *)smem;           // [E]
     float2 *s_vel = s_pos + E;                // [N]
     float2 *s_np = s_vel + N;                 // [N] integrated agent positions
@@ -788,7 +804,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         sym.arow = (uint64_t *)q;
         q += 16 * N * W;
         sym.own = (uint64_t *)q;
-        q += 8 * p.No * W;
+        q += 8 * No * W;
         sym.flag = (int *)q;
     }
     float2 *s_prev = (float2 *)(smem + p.wave_lds_step);   // [E] positions of the previous step
@@ -866,7 +882,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                 }
             }
             float Fx = u.x + fx, Fy = u.y + fy;
-            if (late_params().strict && strict_bad(i, pi, N, late_params().M, [&](int c) { return s_pos[collider_entity(c, N)]; })) {
+            if (late_params().strict && strict_bad(i, pi, N, M, [&](int c) { return s_pos[collider_entity(c, N)]; })) {
                 Fx = __builtin_nanf("");
                 Fy = __builtin_nanf("");
             }
@@ -891,7 +907,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         t += 1;
         const bool done = t >= late_params().EL;
 
-        int pairs = obs_sweep_sym(p, s_pos, sym, s_cost, eb, true, rout, rkeep, s_cm);
+        int pairs = obs_sweep_sym<kN, kNo>(p, s_pos, sym, s_cost, eb, true, rout, rkeep, s_cm);
         auto nonfinite_part = [&]() {
             int bd = 0;
             if (late_params().degenerate)
@@ -947,7 +963,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         if (done && late_params().auto_reset) {
             if (tid == 0) late_params().ep_last[b] = acc;
             relayout();
-            pairs = obs_sweep_sym(p, s_pos, sym, s_cost, eb, false, rout, rkeep, s_cm);
+            pairs = obs_sweep_sym<kN, kNo>(p, s_pos, sym, s_cost, eb, false, rout, rkeep, s_cm);
             pairs = tile_sum(pairs, s_ired);
             bad = tile_sum(nonfinite_part(), s_ired + 3 * kTileWaves);
         }
@@ -1010,8 +1026,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                 ex = (int)min(late_params().ro.cap, (int64_t)0x7fffffff);
             }
             int64_t off;
-            emit_env(p, roll_edge_sink<kSlots>(late_params(), k - 1, K), s_prev, rkeep, tid == 0 ? ex : 0, &off,
-                     s_red, s_scr, kRollTileScr, g0);
+            emit_env<kN, kNo>(p, roll_edge_sink<kSlots>(late_params(), k - 1, K), s_prev, rkeep, tid == 0 ? ex : 0,
+                              &off, s_red, s_scr, kRollTileScr, g0);
             if (tid == 0) {
                 KernargParams &q = late_params();
                 int64_t *const eptr = q.ro.eptr + (kSlots ? (k - 1) * q.ro.ep_s : 0);
@@ -1043,6 +1059,9 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
 
 const void *roll_tile_kernel_fn(const DevParams &p, bool slots) {
     if (p.path != kPathTile || !p.tile_sym) return nullptr;
+    // (a C3-compiled instantiation, <96, 96>, trades the runtime shape's SGPR
+    // spills — 132 -> 106 — for 22 VGPR spills to scratch at the 64-VGPR
+    // budget of 8 waves per SIMD: not used)
     return slots ? reinterpret_cast<const void *>(&gsm_roll_tile_kernel<true>)
                  : reinterpret_cast<const void *>(&gsm_roll_tile_kernel<false>);
 }
