@@ -396,7 +396,8 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
     const bool tile = p.path == gsm::kPathTile;
     const void *fn = tile ? gsm::roll_tile_kernel_fn(p, false) : gsm::roll_seg_kernel_fn(p, false);
     if (!fn) return kEagerIneligible;   // (the action format may differ per call: checked every time)
-    const int nb = tile ? gsm::step_grid_blocks(p) : (p.B + gsm::kWavesPerBlock - 1) / gsm::kWavesPerBlock;
+    const int per_blk = tile ? 1 : gsm::roll_seg_envs_per_block(p);
+    const int nb = tile ? gsm::step_grid_blocks(p) : (p.B + per_blk - 1) / per_blk;
     const size_t lds = tile ? gsm::roll_tile_kernel_lds(p) : gsm::roll_kernel_lds(p);
     if (h->eager_roll < 0) {
         h->eager_roll = 0;
@@ -755,8 +756,10 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         if (per_step[0].edge_index) ro.cap = per_step[0].edge_capacity;
         // p now describes the last slot: the final emit launch writes it
     }
-    // segmented / ragged rollout: one env per wave whatever the config's G (4 per workgroup)
-    const int nb = tile ? gsm::step_grid_blocks(p) : (p.B + gsm::kWavesPerBlock - 1) / gsm::kWavesPerBlock;
+    // segmented / ragged rollout: one env per wave whatever the config's G (4 per workgroup), or four
+    // small envs per wave (16 per workgroup)
+    const int per_blk = tile ? 1 : ragged ? gsm::kWavesPerBlock : gsm::roll_seg_envs_per_block(p);
+    const int nb = tile ? gsm::step_grid_blocks(p) : (p.B + per_blk - 1) / per_blk;
     const size_t roll_lds = tile ? gsm::roll_tile_kernel_lds(p)
                                  : ragged ? gsm::roll_ragged_kernel_lds(p) : gsm::roll_kernel_lds(p);
     // every workgroup resident at once (one residency round; a workgroup only

@@ -178,6 +178,7 @@ const void *emit_seg_kernel_fn(const DevParams &p);
 // fused K-step rollout kernel (nullptr where the config has none: G > 1,
 // runtime shapes, other families) and its LDS bytes
 const void *roll_seg_kernel_fn(const DevParams &p, bool slots);   // slots: a rollout buffer's outputs
+int roll_seg_envs_per_block(const DevParams &p);   // 4 (one env per wave) or 16 (small envs, four per wave)
 size_t roll_kernel_lds(const DevParams &p);
 const void *roll_tile_kernel_fn(const DevParams &p, bool slots);   // nullptr unless p.tile_sym
 size_t roll_tile_kernel_lds(const DevParams &p);

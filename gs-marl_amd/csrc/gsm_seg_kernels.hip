@@ -1656,6 +1656,387 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     }
 }
 
+// ---------------------------------------------------------------------------
+// Fused rollout of SMALL envs (M = N + No <= 16; C2: 3 agents + 3 obstacles),
+// four envs per wave in 16-lane segments. One env per wave left
+// 58 of 64 lanes idle at C2 and paid every per-step wave-level instruction —
+// reductions, stores, the hand-off, most of them on the CU's shared scalar
+// issue path — once per env; here once per four. Lane (seg, m):
+// env (blockIdx * 4 + wave) * 4 + seg, collider row m (agents [0, N), obstacle
+// m >= N = entity N + m). Per-env values live in every lane of the segment;
+// segment sums and scans are 16-lane DPP row operations (plain VALU). The
+// pair sweep forms each row's bits by VGPR integer arithmetic on d2
+// (gsm_ragged_kernels.hip ragged_sweep) over all M columns, so obstacle rows
+// need no cached obstacle-obstacle bits. Every output, the operations and
+// their order are those of gsm_step_seg_kernel + gsm_emit_seg_kernel for the
+// same envs (G = 4 there too: a workgroup holds the same 16 envs, so the last
+// step's workgroup sums are the config's block_edge_sum directly).
+constexpr int kPackSeg = 16, kPackG = kWave / kPackSeg;   // lanes per env, envs per wave
+template <int kN, int kNo>
+constexpr int pack_lds_wave() { return 2 * 8 * kPackG * (2 * kN + kNo) + 8 * kPackG * kN; }
+template <int kCtrl>
+__device__ __forceinline__ int dpp_row0(int v) {   // DPP within 16-lane rows, 0 shifted in
+    return __builtin_amdgcn_update_dpp(0, v, kCtrl, 0xf, 0xf, true);
+}
+__device__ __forceinline__ int seg_sum16(int v) {   // every lane: its 16-lane row's sum
+    v += dpp_row0<0xB1>(v);
+    v += dpp_row0<0x4E>(v);
+    v += dpp_row0<0x141>(v);
+    v += dpp_row0<0x140>(v);
+    return v;
+}
+__device__ __forceinline__ float seg_sum16(float v) {
+    v += __int_as_float(dpp_row0<0xB1>(__float_as_int(v)));
+    v += __int_as_float(dpp_row0<0x4E>(__float_as_int(v)));
+    v += __int_as_float(dpp_row0<0x141>(__float_as_int(v)));
+    v += __int_as_float(dpp_row0<0x140>(__float_as_int(v)));
+    return v;
+}
+__device__ __forceinline__ int seg_scan16(int v) {   // inclusive scan within the 16-lane row
+    v += dpp_row0<0x111>(v);
+    v += dpp_row0<0x112>(v);
+    v += dpp_row0<0x114>(v);
+    v += dpp_row0<0x118>(v);
+    return v;
+}
+
+// (four envs per wave: C2's 4096 envs are 1024 waves, one per SIMD; up to
+// 128 VGPRs, four waves per SIMD, keep 16384 envs in one residency round)
+template <int kN, int kNo, int kFmt, bool kSlots>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void gsm_roll_pack_kernel(DevParams p) {
+    constexpr int N = kN, M = kN + kNo, E = 2 * kN + kNo;
+    static_assert(M <= kPackSeg && E <= kPackSeg, "one 16-lane segment per env");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63, seg = lane >> 4, m = lane & (kPackSeg - 1);
+    const int64_t b = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kPackG + seg;   // this lane's env
+    const bool env_live = b < p.B;
+    const bool live = env_live && m < M, agent = live && m < N;
+    const int64_t eb = env_live ? b : 0;
+    // LDS per wave: positions ping-pong [2][G][E] (step k reads buffer k & 1,
+    // its agents' new positions go to the other; goals and obstacles kept in
+    // both), the next step's forces [G][N]
+    float2 *const s_w = (float2 *)(smem + wave * pack_lds_wave<kN, kNo>());
+    auto pos_buf = [&](int k) { return s_w + (k & 1) * kPackG * E + seg * E; };   // this env's rows
+    float2 *const s_force = s_w + 2 * kPackG * E + seg * N;
+    int *s_bc = (int *)(smem + kWavesPerBlock * pack_lds_wave<kN, kNo>());   // [2][16]: env counts by parity
+    int *s_pre = s_bc + 2 * kWavesPerBlock * kPackG;                          // [2][16]: their exclusive prefix
+    int *s_red = s_pre + 2 * kWavesPerBlock * kPackG;                         // [2]: the workgroup's offset
+    const int ent = m < N ? m : N + m;                                       // this lane's collider entity
+
+    // ---- the state before step t_first
+    const float2 *pos_g = p.pos + eb * E;
+    float2 x = env_live && m < E ? pos_g[m] : make_float2(0.0f, 0.0f);   // lane m: entity m
+    float2 v = agent ? p.vel[eb * N + m] : make_float2(0.0f, 0.0f);
+    int t = env_live ? p.step_count[eb] : 0, ep = env_live ? p.episode[eb] : 0;
+    float2 acc = env_live ? p.ep_acc[eb] : make_float2(0.0f, 0.0f);
+    uint32_t cand_prev = agent ? (uint32_t)p.contact_mask[eb * N + m] : 0u;
+    const float4 a0 = roll_action_load<kN, kFmt>(p, p.roll.t_first % p.roll.n_actions, eb, agent ? m : 0);
+    if (env_live && m < E) pos_buf(0)[m] = pos_buf(1)[m] = x;
+    wave_sync();
+
+    // one pass over the env's M columns from the positions at `s` (lane m:
+    // row m): radius row bits, contact candidates (agent rows), collisions
+    // (agent rows, own column excluded), an agent-column coincidence; with
+    // kForce the contact forces of the candidates added to *F in ascending
+    // collider order (the step kernel's force pass: same operations)
+    auto sweep = [&](const float2 *sp, float2 pm, uint32_t &rad, uint32_t &cand, int &cnt, bool &zero_agent,
+                     float2 *F) {
+        KernargParams &q = late_params();
+        uint32_t r2b1 = __float_as_uint(q.R2) + 1u;
+        uint32_t cutb = __float_as_uint(m < N ? q.cut2_aa : q.cut2_ao);   // this row's partner class: see below
+        asm volatile("" : "+v"(r2b1), "+v"(cutb));
+        // (the candidate threshold is the PAIR's: agent-agent for agent columns
+        // of an agent row, agent-obstacle otherwise)
+        uint32_t cut_aa = __float_as_uint(q.cut2_aa), cut_ao = __float_as_uint(q.cut2_ao);
+        asm volatile("" : "+v"(cut_aa), "+v"(cut_ao));
+        (void)cutb;
+        uint32_t rw = 0, cw = 0, nz = 0;
+#pragma unroll
+        for (int c = M - 1; c >= 0; --c) {   // descending: column c ends at bit c
+            const float2 qc = sp[c < N ? c : N + c];
+            const float dx = pm.x - qc.x, dy = pm.y - qc.y;
+            const uint32_t a = __float_as_uint(__builtin_fabsf(dx * dx) + __builtin_fabsf(dy * dy));
+            const uint32_t na = 0u - a;
+            const uint32_t cb = (c < N && m < N) ? cut_aa : cut_ao;   // c compile-time; m < N per lane
+            rw = __builtin_amdgcn_alignbit(rw, na & (a - r2b1), 31);
+            cw = __builtin_amdgcn_alignbit(cw, na & (a - cb), 31);
+            nz = __builtin_amdgcn_alignbit(nz, na, 31);
+        }
+        constexpr uint32_t colmask = (1u << M) - 1u, amask = (1u << N) - 1u;
+        const uint32_t self = 1u << m;
+        const uint32_t zero = ~nz & colmask & ~self;
+        zero_agent = live && (zero & amask) != 0u;
+        rad = live ? rw & colmask : 0u;
+        cand = agent ? cw & colmask : 0u;
+        int n = agent ? __popc(zero) : 0;
+        if (agent) {
+            float Fx = F ? F->x : 0.0f, Fy = F ? F->y : 0.0f;
+            const float dmin2_aa = q.dmin2_aa, dmin2_ao = q.dmin2_ao, dmin_aa = q.dmin_aa, dmin_ao = q.dmin_ao;
+            for (uint32_t w = cand; w; w &= w - 1u) {
+                const int c = __builtin_ctz(w);
+                const bool ag = c < N;
+                const float2 qc = sp[ag ? c : N + c];
+                const float dx = pm.x - qc.x, dy = pm.y - qc.y;
+                const float d2 = dx * dx + dy * dy;
+                n += d2 < (ag ? dmin2_aa : dmin2_ao) ? 1 : 0;
+                if (F) {
+                    const float f = contact_scale(q, d2, ag ? dmin_aa : dmin_ao);
+                    Fx += f * dx;
+                    Fy += f * dy;
+                }
+            }
+            if (F) *F = make_float2(Fx, Fy);
+        }
+        cnt = n;
+    };
+
+    {   // the forces of step t_first: its action, then the stored candidates
+        float2 F = roll_force<kFmt>(late_params(), a0, agent);
+        if (agent) {
+            const float2 pi = x;   // lane m < N: agent m = entity m
+            const float dmin_aa = late_params().dmin_aa, dmin_ao = late_params().dmin_ao;
+            for (uint32_t w = cand_prev; w; w &= w - 1u) {
+                const int c = __builtin_ctz(w);
+                const bool ag = c < N;
+                const float2 pj = pos_buf(0)[ag ? c : N + c];
+                const float dx = pi.x - pj.x, dy = pi.y - pj.y;
+                const float d2 = dx * dx + dy * dy;
+                const float f = contact_scale(late_params(), d2, ag ? dmin_aa : dmin_ao);
+                F.x += f * dx;
+                F.y += f * dy;
+            }
+            s_force[m] = F;
+        }
+    }
+
+    const int K = p.roll.K, n_act = p.roll.n_actions;
+    const uint32_t etag = roll_epoch_tag(p.roll.epoch);
+    int arow = p.roll.t_first % n_act;
+    uint32_t row_prev = 0;       // the previous step's radius row bits (emitted one iteration on)
+    uint32_t cand_keep = cand_prev;
+    bool coinc = false;
+    const int slot = wave * kPackG + seg;   // this env's index in the workgroup
+
+    // the edges of the step before iteration k (positions pos_buf(k), rows
+    // row_prev) at the offset of the look-back (every wave of the workgroup)
+    auto emit_prev = [&](const int k) {
+        const int par = k & 1;
+        const int *cb = s_bc + (1 - par) * kWavesPerBlock * kPackG;
+        if (wave == 0) {
+            KernargParams &qe = late_params();
+            const int64_t kb = (int64_t)(k - 1) * gridDim.x;
+            const int ex = roll_lookback(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
+                                         etag | (uint32_t)k, qe.roll.status, lane);
+            if (lane == 0) {
+                int tot = 0;
+#pragma unroll
+                for (int j = 0; j < kWavesPerBlock * kPackG; ++j) tot += cb[j];
+                s_red[0] = ex;
+                __hip_atomic_store((gu64 *)(qe.roll.gran + (int64_t)K * gridDim.x + kb + blockIdx.x),
+                                   ((uint64_t)(etag | (uint32_t)k) << 32) | (uint32_t)(ex + tot), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        __syncthreads();
+        int64_t env_off = (int64_t)s_red[0] + s_pre[(1 - par) * kWavesPerBlock * kPackG + slot];
+        const int my_cnt = cb[slot];
+        if (env_off < 0) {   // a broken hand-off: never write out of bounds
+            if (lane == 0)
+                __hip_atomic_store((gu32 *)late_params().roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            env_off = late_params().ro.cap;
+        }
+        KernargParams &qs = late_params();
+        if (env_live && m == 0) {
+            int64_t *const eptr = qs.ro.eptr + (kSlots ? (k - 1) * qs.ro.ep_s : 0);
+            eptr[b] = env_off;
+            if (b == qs.B - 1) eptr[qs.B] = env_off + my_cnt;
+        }
+        // rows in entity order: agent rows (agent columns, own goal, obstacle
+        // columns), goal rows, obstacle rows (agent then obstacle columns)
+        const int c = live ? __popc(row_prev) + (agent ? 1 : 0) : 0;
+        const int incl = seg_scan16(c);
+        const int a_total = seg_sum16(agent ? c : 0);
+        const EdgeSink out = roll_edge_sink<kSlots>(qs, k - 1, K);
+        const float2 *sp = pos_buf(k);
+        const int32_t g0 = (int32_t)(eb * E);
+        if (live) {
+            int64_t o = env_off + (incl - c) + (m >= N ? N : 0);
+            const float2 a = sp[ent];
+            auto put = [&](int64_t at, int dst) {
+                if (at < out.cap) {
+                    const float2 qd = sp[dst];
+                    const float dx = a.x - qd.x, dy = a.y - qd.y;
+                    out.index[at] = g0 + ent;
+                    out.index[out.cap + at] = g0 + dst;
+                    out.attr[at] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+                }
+            };
+            constexpr uint32_t amask = (1u << N) - 1u;
+            for (uint32_t w = row_prev & amask; w; w &= w - 1u) put(o++, __builtin_ctz(w));
+            if (agent) {
+                put(o++, N + m);                                     // agent m -> its goal
+                const float2 g = sp[N + m];
+                const float dx = g.x - a.x, dy = g.y - a.y;
+                const int64_t at = env_off + a_total + m;            // goal row: goal m -> agent m
+                if (at < out.cap) {
+                    out.index[at] = g0 + N + m;
+                    out.index[out.cap + at] = g0 + m;
+                    out.attr[at] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+                }
+            }
+            for (uint32_t w = row_prev & ~amask; w; w &= w - 1u) put(o++, N + __builtin_ctz(w));
+        }
+        wave_sync();
+    };
+
+    for (int k = 0; k < K; ++k) {
+        const int nrow = arow + 1 == n_act ? 0 : arow + 1;
+        const float4 anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, agent ? m : 0);
+        const float2 *const s_cur = pos_buf(k);
+        float2 *const s_pos = pos_buf(k + 1);
+        KernargParams &pc = late_params();
+        // apply_environment_force (formed by the previous sweep) + integrate_state
+        if (agent) {
+            const float2 pi = s_cur[m];
+            const float2 F0 = s_force[m];
+            float Fx = F0.x, Fy = F0.y;
+            if (pc.strict && strict_bad(m, pi, N, M, [&](int c) { return s_cur[c < N ? c : N + c]; })) {
+                Fx = __builtin_nanf("");
+                Fy = __builtin_nanf("");
+            }
+            const float dt = pc.dt, max_speed = pc.max_speed;
+            v.x = v.x * pc.omd;
+            v.y = v.y * pc.omd;
+            v.x = v.x + (Fx * pc.inv_mass) * dt;
+            v.y = v.y + (Fy * pc.inv_mass) * dt;
+            if (max_speed > 0.0f) {
+                const float sp = sqrtf(v.x * v.x + v.y * v.y);
+                if (sp > max_speed) {
+                    v.x = v.x / sp * max_speed;
+                    v.y = v.y / sp * max_speed;
+                }
+            }
+            s_pos[m] = make_float2(pi.x + v.x * dt, pi.y + v.y * dt);
+        }
+        wave_sync();
+        t += 1;
+        const bool done = env_live && t >= pc.EL;
+
+        // observation on the post-physics positions (and the next step's forces)
+        float2 pm = live ? s_pos[ent] : make_float2(0.0f, 0.0f);
+        uint32_t rad, cand;
+        int cnt;
+        bool za;
+        float2 Fn = roll_force<kFmt>(late_params(), anext, agent);
+        sweep(s_pos, pm, rad, cand, cnt, za, &Fn);
+        // reward / cost
+        float r = 0.0f;
+        if (agent) {
+            const float2 g = s_pos[N + m];
+            const float dx = pm.x - g.x, dy = pm.y - g.y;
+            r = -__builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+        }
+        float rsum = seg_sum16(r);
+        const int csum = seg_sum16(agent ? cnt : 0);
+        {
+            KernargParams &q = late_params();
+            if (agent) {
+                (q.ro.rew + (kSlots ? k * q.ro.rc_s : 0) + eb * N)[m] = q.shared_reward ? rsum : r;
+                (q.ro.cost + (kSlots ? k * q.ro.rc_s : 0) + eb * N)[m] = (float)cnt;
+            }
+            if (q.shared_reward) rsum *= (float)N;
+        }
+        if (env_live) {
+            acc.x += rsum;
+            acc.y += (float)csum;
+        }
+        const bool reset = done && late_params().auto_reset;
+        if (reset && m == 0) late_params().ep_last[b] = acc;
+        if (__any(reset)) {
+            // auto-reset: scenario.reset_world for the segments whose env is done
+            if (reset) {
+                ep = ep + 1;
+                t = 0;
+                acc = make_float2(0.0f, 0.0f);
+                v = make_float2(0.0f, 0.0f);
+                const uint32_t gid = (uint32_t)(late_params().env_base + b);
+                if (m < E) s_pos[m] = layout_pos(p, gid, (uint32_t)ep, (uint32_t)m);
+            }
+            wave_sync();
+            if (reset) {
+                pm = live ? s_pos[ent] : make_float2(0.0f, 0.0f);
+                Fn = roll_force<kFmt>(late_params(), anext, agent);
+                sweep(s_pos, pm, rad, cand, cnt, za, &Fn);
+            }
+        }
+        coinc = (seg_sum16(za ? 1 : 0) != 0);
+        if (agent) s_force[m] = Fn;
+
+        // node features: agent rows every step, goal / obstacle rows on a new layout
+        KernargParams &q = late_params();
+        const bool statics = q.nf_full || reset;
+        float *nf = q.ro.nf + (kSlots ? k * q.ro.nf_s : 0) + eb * E * 7;
+        if (agent) {
+            const float2 g = s_pos[N + m];
+            store_row(nf + m * 7, v, pm, make_float2(g.x - pm.x, g.y - pm.y), 0.0f);
+        }
+        if (env_live && statics && m >= N && m < E) {
+            const float2 a = s_pos[m];
+            store_row(nf + m * 7, make_float2(0.0f, 0.0f), a, make_float2(0.0f, 0.0f), m < 2 * N ? 1.0f : 2.0f);
+        }
+        const int edges = seg_sum16(live ? (int)__popc(rad) : 0) + 2 * N;
+        if (env_live && m == 0) {
+            (q.ro.done + (kSlots ? k * q.ro.done_s : 0))[b] = done ? 1 : 0;
+            if (kSlots || k == K - 1) (q.ro.ecount + (kSlots ? k * q.ro.ec_s : 0))[b] = edges;
+        }
+
+        // publish the workgroup's edge sum of this step
+        const int par = k & 1;
+        if (m == 0) s_bc[par * kWavesPerBlock * kPackG + slot] = env_live ? edges : 0;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int sum = 0;
+            for (int j = 0; j < kWavesPerBlock * kPackG; ++j) {
+                s_pre[par * kWavesPerBlock * kPackG + j] = sum;
+                sum += s_bc[par * kWavesPerBlock * kPackG + j];
+            }
+            __hip_atomic_store((gu64 *)(q.roll.gran + (int64_t)k * gridDim.x + blockIdx.x),
+                               ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)sum, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            if (k == K - 1) q.block_edge_sum[blockIdx.x] = sum;   // the config's G = 4 workgroup layout
+        }
+        if (k > 0) emit_prev(k);
+        row_prev = rad;
+        cand_keep = cand;
+        if (__builtin_expect(__any(reset), 0)) {   // the new episode's statics into the other buffer
+            if (reset && m >= N && m < E) pos_buf(k)[m] = s_pos[m];
+        }
+        arow = nrow;
+        wave_sync();
+    }
+    emit_prev(K);   // the tail: the last step's edges
+    // the final state (what the next launch or an eager step reads)
+    KernargParams &q = late_params();
+    const float2 *const s_fin = pos_buf(K);
+    if (env_live && m < E) q.pos[eb * E + m] = s_fin[m];
+    if (agent) {
+        q.vel[eb * N + m] = v;
+        q.contact_mask[eb * N + m] = cand_keep;
+    }
+    if (live) q.row_mask[eb * M + m] = row_prev;
+    if (env_live && m == 0) {
+        q.step_count[b] = t;
+        q.episode[b] = ep;
+        q.ep_acc[b] = acc;
+    }
+    if (q.degenerate) {
+        const bool nf_agent = agent && nonfinite2(s_fin[m]);
+        const bool nfe = seg_sum16(nf_agent ? 1 : 0) != 0;
+        if (env_live && m == 0) q.degenerate[b] = (uint8_t)((coinc ? kDegCoincident : 0) | (nfe ? kDegNonfinite : 0));
+    }
+}
+
 // Specialisations with compile-time shapes (segment arithmetic folded, G = 1
 // collectives for 24 agents) and action formats; anything else runs the
 // runtime-shape instantiation.
@@ -1681,8 +2062,28 @@ static const void *pick_step_seg(const DevParams &p) {
 const void *step_seg_kernel_fn(const DevParams &p) { return pick_step_seg<false>(p); }
 const void *lag_step_seg_kernel_fn(const DevParams &p) { return pick_step_seg<true>(p); }
 
+// small shapes run four envs per wave (gsm_roll_pack_kernel)
+#define GSM_PACK_SHAPES(X) X(3, 3)
+static bool roll_packed(const DevParams &p) {
+#define GSM_PICK(n, no) if (p.N == n && p.No == no) return true;
+    GSM_PACK_SHAPES(GSM_PICK)
+#undef GSM_PICK
+    return false;
+}
+int roll_seg_envs_per_block(const DevParams &p) { return roll_packed(p) ? kWavesPerBlock * kPackG : kWavesPerBlock; }
+
 template <bool kSlots>
 static const void *pick_roll_seg(const DevParams &p) {
+#define GSM_PICK(n, no)                                                                            \
+    if (p.N == n && p.No == no) {                                                                  \
+        switch (p.action_fmt) {                                                                    \
+            case 0: return reinterpret_cast<const void *>(&gsm_roll_pack_kernel<n, no, 0, kSlots>); \
+            case 1: return reinterpret_cast<const void *>(&gsm_roll_pack_kernel<n, no, 1, kSlots>); \
+            default: return reinterpret_cast<const void *>(&gsm_roll_pack_kernel<n, no, 2, kSlots>); \
+        }                                                                                          \
+    }
+    GSM_PACK_SHAPES(GSM_PICK)
+#undef GSM_PICK
 #define GSM_PICK(n, no)                                                                          \
     if (p.N == n && p.No == no) {                                                                \
         switch (p.action_fmt) {                                                                  \
@@ -1700,6 +2101,10 @@ const void *roll_seg_kernel_fn(const DevParams &p, bool slots) {
     return slots ? pick_roll_seg<true>(p) : pick_roll_seg<false>(p);
 }
 size_t roll_kernel_lds(const DevParams &p) {
+#define GSM_PICK(n, no) \
+    if (p.N == n && p.No == no) return (size_t)kWavesPerBlock * pack_lds_wave<n, no>() + 4 * (4 * kWavesPerBlock * kPackG + 2);
+    GSM_PACK_SHAPES(GSM_PICK)
+#undef GSM_PICK
     return (size_t)kWavesPerBlock * roll_lds_wave(p.N, p.E) + 4 * (4 * kWavesPerBlock + 2);
 }
 
