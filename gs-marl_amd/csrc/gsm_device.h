@@ -385,44 +385,29 @@ __device__ __forceinline__ void xfer_grp_publish(const Xfer &x, uint64_t l, int 
 // of those in between), otherwise the window's aggregates are added and the
 // walk moves on. Aggregates were published an iteration earlier, so the walk
 // never waits on an inclusive prefix; an aggregate read early is re-polled.
-// Windows are read kLookbackBatch at a time (all their loads issued before
-// the first is used), so a walk over many windows pays one load latency per
-// batch instead of one per window: in lockstep every workgroup looks back at
-// once and the nearest published inclusive prefix can be many windows away.
-#ifndef GSM_LOOKBACK_BATCH   // A/B (temporary)
-#define GSM_LOOKBACK_BATCH 4
-#endif
-constexpr int kLookbackBatch = GSM_LOOKBACK_BATCH;
+// (Reading several windows per round before using the first, so a long walk
+// pays one load latency per round, measured slower at H: 10.2 vs 9.8 us per
+// step for four windows)
 __device__ __forceinline__ int roll_lookback(const uint64_t *agg_k, const uint64_t *inc_k, uint32_t tag,
                                              uint32_t *status, int lane) {
     int acc = 0;
     int first = (int)blockIdx.x;
     asm volatile("" : "+s"(first));   // no window predicates hoisted into a rollout's loop (SGPR pairs)
-    for (int hi = first; hi > 0; hi -= kWave * kLookbackBatch) {
-        uint64_t xi[kLookbackBatch], xa[kLookbackBatch];
-#pragma unroll
-        for (int u = 0; u < kLookbackBatch; ++u) {
-            const int idx = hi - 1 - lane - u * kWave;      // lane 0 = nearest predecessor of window u
-            const int ci = idx >= 0 ? idx : 0;
-            xi[u] = __hip_atomic_load((const gu64 *)(inc_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            xa[u] = __hip_atomic_load((const gu64 *)(agg_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-#pragma unroll
-        for (int u = 0; u < kLookbackBatch; ++u) {
-            const int idx = hi - 1 - lane - u * kWave;
-            const int ci = idx >= 0 ? idx : 0;
-            const bool valid = idx >= 0;
-            const uint64_t have = __ballot(valid && (uint32_t)(xi[u] >> 32) == tag);
-            const int j = have ? __builtin_ctzll(have) : kWave;   // wave-uniform
-            // aggregates of lanes < j (all valid lanes when no inclusive was found)
-            const bool need = valid && lane < j;
-            uint64_t a = xa[u];
-            if (need && (uint32_t)(a >> 32) != tag) a = roll_wait(agg_k + ci, tag, status);
-            int v = need ? (int)(uint32_t)a : 0;
-            if (lane == j) v = (int)(uint32_t)xi[u];
-            acc += wave_total(v);
-            if (have || hi - (u + 1) * kWave <= 0) return acc;
-        }
+    for (int hi = first; hi > 0; hi -= kWave) {
+        const int idx = hi - 1 - lane;                      // lane 0 = nearest predecessor
+        const int ci = idx >= 0 ? idx : 0;
+        const bool valid = idx >= 0;
+        const uint64_t xi = __hip_atomic_load((const gu64 *)(inc_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t a = __hip_atomic_load((const gu64 *)(agg_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t have = __ballot(valid && (uint32_t)(xi >> 32) == tag);
+        const int j = have ? __builtin_ctzll(have) : kWave;   // wave-uniform
+        // aggregates of lanes < j (all valid lanes when no inclusive was found)
+        const bool need = valid && lane < j;
+        if (need && (uint32_t)(a >> 32) != tag) a = roll_wait(agg_k + ci, tag, status);
+        int v = need ? (int)(uint32_t)a : 0;
+        if (lane == j) v = (int)(uint32_t)xi;
+        acc += wave_total(v);
+        if (have) return acc;
     }
     return acc;
 }

@@ -306,135 +306,6 @@ __device__ __forceinline__ void obs_sweep_g1(const Params &p, const Lane &L, con
     ccnt = cc;
 }
 
-// One env per wave (32 < M <= 64, compile-time even N <= 32, No <= 32): the
-// same outputs as obs_sweep_g1 with no instruction on the CU's scalar issue
-// path inside the column loop (compares, ballots, lane writes and SGPR
-// operands all issue there, ~1 per CU and cycle for its four SIMDs:
-// tools/probe_issue.hip):
-//   * per agent column j, every row m forms its own bits by integer
-//     arithmetic on a = bits(|dx*dx| + |dy*dy|) (gsm_ragged_kernels.hip
-//     ragged_sweep): 0 < d2 <= R2 as sign(-a & (a - bits(R2) - 1)) and
-//     d2 < cut2 (candidates plus self and coincident pairs) as sign(a -
-//     bits(cut2)), shifted into the row word with one v_alignbit each;
-//   * an agent row's obstacle-column bits are the transpose of the obstacle
-//     rows' agent-column words: those go through LDS, and agent lane j takes
-//     bit j of each (a shift and a v_alignbit per obstacle);
-//   * the walk over each agent row's near bits (collisions, coincident pairs,
-//     kForce: the next step's contact forces) is obs_sweep_g1's.
-template <int kN, int kNo, bool kForce = false, typename FInit = int, typename Params = DevParams>
-__device__ __forceinline__ void obs_sweep_lane(const Params &p, const Lane &L, const float2 *sp, float *s_xy,
-                                               float2 pm, bool full, uint64_t oo, uint64_t &row, uint64_t &cand,
-                                               int &ccnt, bool &coinc, float2 *force = nullptr, FInit finit = 0) {
-    typedef float f32x2 __attribute__((ext_vector_type(2)));
-    constexpr int N = kN, No = kNo, M = kN + kNo;
-    static_assert(M > 32 && M <= 64 && N <= 32 && N % 2 == 0 && No <= 32, "one env per wave, 32-bit halves");
-    constexpr uint64_t abits = (1ull << N) - 1;
-    const bool obst = L.live && L.m >= N;
-    if (L.agent) {
-        const int at = (L.m >> 1) * 4 + (L.m & 1);
-        s_xy[at] = pm.x;
-        s_xy[at + 2] = pm.y;
-    }
-    if (!L.live) pm = make_float2(1.0e18f, 1.0e18f);        // d2 ~ 1e36: every predicate false
-    uint32_t r2b1 = __float_as_uint(p.R2) + 1u;
-    uint32_t cutb = __float_as_uint(obst ? p.cut2_ao : p.cut2_aa);
-    asm volatile("" : "+v"(r2b1), "+v"(cutb));               // VGPR operands in the column loop
-    uint32_t rad = 0, near = 0;                              // bit j: agent column j
-    wave_sync();
-    const f32x2 px = {pm.x, pm.x}, py = {pm.y, pm.y};
-    const float4 *xy4 = (const float4 *)s_xy;
-    auto col = [&](float d2) {
-        const uint32_t a = __float_as_uint(d2);
-        rad = __builtin_amdgcn_alignbit(rad, (0u - a) & (a - r2b1), 31);
-        near = __builtin_amdgcn_alignbit(near, a - cutb, 31);
-    };
-#pragma unroll
-    for (int g = N / 2 - 1; g >= 0; --g) {                   // descending: column j ends at bit j
-        const float4 Q = xy4[g];
-        const f32x2 dx = px - (f32x2){Q.x, Q.y};
-        const f32x2 dy = py - (f32x2){Q.z, Q.w};
-        const f32x2 sx = dx * dx, sy = dy * dy;
-        col(__builtin_fabsf(sx.y) + __builtin_fabsf(sy.y));  // column 2g + 1
-        col(__builtin_fabsf(sx.x) + __builtin_fabsf(sy.x));  // column 2g
-    }
-    // the transpose: obstacle row N + k's agent words -> bit k of agent rows
-    uint32_t *s_tr = (uint32_t *)(s_xy + 2 * N);             // [2][64] after the column pairs
-    s_tr[L.lane] = rad;
-    s_tr[kWave + L.lane] = near;
-    wave_sync();
-    uint32_t orad = 0, onear = 0;
-    const uint32_t sh = (uint32_t)(31 - L.m) & 31u;          // agent lane m: bit m to bit 31
-    const uint4 *tr4 = (const uint4 *)s_tr;
-    static_assert(N % 4 == 0, "obstacle words read as uint4 from word N");
-#pragma unroll
-    for (int k4 = (No - 1) / 4; k4 >= 0; --k4) {
-        const uint4 R = tr4[(N >> 2) + k4], C = tr4[((kWave + N) >> 2) + k4];
-        const uint32_t rw[4] = {R.x, R.y, R.z, R.w}, cw[4] = {C.x, C.y, C.z, C.w};
-#pragma unroll
-        for (int u = 3; u >= 0; --u) {
-            if (4 * k4 + u >= No) continue;
-            orad = __builtin_amdgcn_alignbit(orad, rw[u] << sh, 31);
-            onear = __builtin_amdgcn_alignbit(onear, cw[u] << sh, 31);
-        }
-    }
-    uint64_t r, nr = 0;
-    if (L.agent) {
-        r = (uint64_t)rad | ((uint64_t)orad << N);
-        nr = ((uint64_t)near | ((uint64_t)onear << N)) & ~(1ull << L.m);   // self dropped
-    } else {
-        r = obst ? (((!full ? oo : 0ull) & ~abits) | rad) : 0ull;
-    }
-    if (full) {
-        // obstacle columns: obstacle-obstacle bits (the agent-obstacle bits
-        // of agent rows came through the transpose)
-#pragma unroll 2
-        for (int k = N; k < M; ++k) {
-            const float2 q = sp[N + k];
-            const float dx = pm.x - q.x, dy = pm.y - q.y;
-            const float d2 = dx * dx + dy * dy;
-            if (obst && d2 > 0.0f && d2 <= p.R2) r |= 1ull << k;
-        }
-    }
-    // collisions and contact candidates of agent rows from the near bits
-    int cc = 0;
-    uint64_t c = 0;
-    bool coincident = false;
-    if (L.agent) {
-        uint64_t w = nr;
-        c = w;
-        float Fx = 0.0f, Fy = 0.0f;
-        if constexpr (kForce) {
-            const float2 f0 = finit();
-            Fx = f0.x;
-            Fy = f0.y;
-        }
-        const float dmin_aa = p.dmin_aa, dmin_ao = p.dmin_ao;   // both read before the walk
-        while (w) {
-            const int k = __builtin_ctzll(w);
-            w &= w - 1;
-            const float2 q = sp[k < N ? k : N + k];
-            const float dx = pm.x - q.x, dy = pm.y - q.y;
-            const float d2 = dx * dx + dy * dy;
-            cc += d2 < (k < N ? p.dmin2_aa : p.dmin2_ao) ? 1 : 0;
-            if (d2 == 0.0f) {
-                c &= ~(1ull << k);
-                coincident = true;
-            } else if (kForce) {
-                const float f = contact_scale(p, d2, k < N ? dmin_aa : dmin_ao);
-                Fx += f * dx;
-                Fy += f * dy;
-            }
-        }
-        if constexpr (kForce) *force = make_float2(Fx, Fy);
-    }
-    // an obstacle row coincident with an agent: its agent bit is absent from
-    // rad (exact predicate), and the agent's walk sees the pair
-    coinc = __any(coincident);
-    row = r;
-    cand = c;
-    ccnt = cc;
-}
-
 // Observation sweep (file header). row/cand/ccnt are per lane: row = radius
 // row mask (compact bits), cand = contact candidates (agent lanes),
 // ccnt = collisions of agent lanes (self excluded), coinc = the lane's env
@@ -454,11 +325,10 @@ __device__ __forceinline__ void obs_sweep(const Params &p, const Shape<kN, kNo> 
                                           float2 *force = nullptr, FInit finit = 0) {
     static_assert(!kForce || sweep_walks_near<kN, kNo>(kG), "contact forces only in the near-bit walk");
     if constexpr (sweep_walks_near<kN, kNo>(kG)) {
-#ifdef GSM_SWEEP_BALLOT   // A/B of the ballot sweep (temporary)
+        // (a variant forming each row's bits by VGPR integer arithmetic, off the
+        // scalar issue path as the ragged sweep does, measured slower here:
+        // 10.2 vs 9.0 us per step at H)
         obs_sweep_g1<kN, kNo, kForce>(p, L, sp, s_xy, pm, full, oo, row, cand, ccnt, coinc, force, finit);
-#else
-        obs_sweep_lane<kN, kNo, kForce>(p, L, sp, s_xy, pm, full, oo, row, cand, ccnt, coinc, force, finit);
-#endif
         return;
     }
     const int N = s.N, M = s.M;
@@ -1336,6 +1206,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     constexpr int scr_cap = (kStep - 8 * E) / 4;
     const bool wave_live = L0.b < p.B;
     const int64_t eb = wave_live ? L0.b : 0;
+    GSM_RSTAMP(p, L0.b, 0);   // diagnostic builds: the launch's timeline per wave
 
     // ---- the state before step t_first and step t_first's actions
     // (p.actions); the edges of that state were emitted by whatever ran before
@@ -1349,6 +1220,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         if (L0.lane + kWave < E) s_buf0[L0.lane + kWave] = s_buf1[L0.lane + kWave] = in.x1;
     }
     wave_sync();
+    GSM_RSTAMP(p, L0.b, 1);
     // apply_environment_force: the action force plus the contact terms of the
     // candidates in ascending collider order
     auto add_contacts = [&](const float2 *s_pos, float2 F, float2 pi, uint64_t cm, const KernargParams &pc) {
@@ -1405,6 +1277,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             }
         }
         __syncthreads();
+        if (k == K) GSM_RSTAMP(p, L.b, 6);
         // (the prefix formed once by thread 0, not w < wave selects: those
         // are loop-invariant lane masks the compiler holds in SGPR pairs)
         const int before = s_pre[(1 - par) * kWavesPerBlock + wave];
@@ -1483,6 +1356,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             s_pos[m] = np;
         }
         wave_sync();
+        if (k == 0) GSM_RSTAMP(p, L.b, 2);
         t += 1;
         const bool done = L.live && t >= pc.EL;
 
@@ -1496,6 +1370,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         float2 Fn = make_float2(0.0f, 0.0f);
         obs_sweep<kN, kNo, 1, kFused>(late_params(), s, L, s_pos, s_nf, pm, false, oo, row, cand, ccnt, coinc, &Fn,
                                       unext);
+        if (k == 0) GSM_RSTAMP(p, L.b, 3);
 
         // reward / cost
         float r = 0.0f;
@@ -1619,6 +1494,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
                 }
             }
         }
+        if (k == K - 1) GSM_RSTAMP(p, L.b, 4);
         if (k > 0) emit_prev(k, L);
         // keep step t for the next iteration's emission and sweep
         oo = row;
@@ -1633,7 +1509,9 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     {   // the tail: the last step's edges
         Lane L = L0;
         asm volatile("" : "+v"(L.lane), "+v"(L.m));
+        GSM_RSTAMP(p, L.b, 5);
         emit_prev(K, L);
+        GSM_RSTAMP(p, L.b, 7);
     }
     // the final state (what the next launch or an eager step reads)
     KernargParams &q = late_params();
@@ -1654,6 +1532,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             if (q.degenerate) q.degenerate[L0.b] = deg;
         }
     }
+    GSM_RSTAMP(p, L0.b, 8);
 }
 
 // ---------------------------------------------------------------------------

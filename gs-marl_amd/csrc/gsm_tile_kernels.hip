@@ -222,6 +222,7 @@ __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s
     __syncthreads();
     const float R2 = p.R2;
     const int U = W * NB8;
+    GSM_TNOW(ts0);
     for (int u = wave; u < U; u += kTileWaves) {
         const int c = u / NB8, jb = u - c * NB8;
         const int m = 64 * c + lane;
@@ -260,6 +261,7 @@ __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s
         // obstacle row m, agent columns j0.. j0+nc-1: byte jb of its words
         if (obst) ((uint8_t *)(S.own + (int64_t)(m - N) * W))[jb] = (uint8_t)(__builtin_bitreverse32(own) >> (32 - nc));
     }
+    GSM_ACC(p, blockIdx.x * kTileWaves + wave, 1, ts0);   // diagnostic builds: column pass
     __syncthreads();
     uint64_t *const rmask = rout ? rout : p.row_mask + eb * M * W;
     const uint64_t *const rprev = rkeep ? rkeep : rmask;
@@ -836,12 +838,16 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     // kernarg view at their use (late_params()): read from `p` the compiler
     // hoists them out of the loop and holds them in SGPRs, spilled to VGPR
     // lanes at 8 waves per SIMD (gsm_roll_seg_kernel).
+    GSM_RSTAMP(p, b * kTileWaves + (tid >> 6), 8);
     for (int k = 0; k <= K; ++k) {
         // thread-derived values re-formed every iteration (an asm barrier): held
         // across the loop their hoisted addresses would pin VGPRs
         int tid = (int)threadIdx.x;
         asm volatile("" : "+v"(tid));
         const int wave = tid >> 6, lane = tid & 63;
+        const int wid = b * kTileWaves + wave;   // (diagnostic stamps)
+        (void)wid;
+        GSM_TNOW(tp0);
         uint64_t *const rout = s_rm + (k & 1) * M * W;
         const uint64_t *const rkeep = s_rm + ((k + 1) & 1) * M * W;   // the previous step's masks
         int edges = 0;
@@ -906,8 +912,11 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         __syncthreads();
         t += 1;
         const bool done = t >= late_params().EL;
-
+        GSM_ACC(late_params(), wid, 0, tp0);   // physics
+        GSM_TNOW(tp1);
         int pairs = obs_sweep_sym<kN, kNo>(p, s_pos, sym, s_cost, eb, true, rout, rkeep, s_cm);
+        GSM_ACC(late_params(), wid, 2, tp1);   // sweep (column pass: 1)
+        GSM_TNOW(tp2);
         auto nonfinite_part = [&]() {
             int bd = 0;
             if (late_params().degenerate)
@@ -960,6 +969,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         }
         acc.x += rsum;
         acc.y += (float)csum;
+        GSM_ACC(late_params(), wid, 3, tp2);   // reward / cost and the exchange
         if (done && late_params().auto_reset) {
             if (tid == 0) late_params().ep_last[b] = acc;
             relayout();
@@ -968,6 +978,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             bad = tile_sum(nonfinite_part(), s_ired + 3 * kTileWaves);
         }
         // the step's observation outputs: agent node rows, static rows on a new layout
+        GSM_TNOW(tp3);
         float *nf = late_params().ro.nf + (kSlots ? k * late_params().ro.nf_s : 0) + eb * E * 7;
         const bool full = relaid || late_params().nf_full;
         for (int i = tid; i < N; i += kTileBlock) {
@@ -1003,10 +1014,12 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                                ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)edges, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
+        GSM_ACC(late_params(), wid, 4, tp3);   // node features, publish
         }   // k < K
         // the previous step's edges at the offset of the look-back
         if (k > 0) {
             int ex = 0;
+            GSM_TNOW(tp4);
             if (wave == 0) {
                 const int64_t kb = (int64_t)(k - 1) * gridDim.x;
                 KernargParams &q = late_params();
@@ -1025,9 +1038,12 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                 __hip_atomic_store((gu32 *)late_params().roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 ex = (int)min(late_params().ro.cap, (int64_t)0x7fffffff);
             }
+            GSM_ACC(late_params(), wid, 5, tp4);   // look-back (wave 0)
+            GSM_TNOW(tp5);
             int64_t off;
             emit_env<kN, kNo>(p, roll_edge_sink<kSlots>(late_params(), k - 1, K), s_prev, rkeep, tid == 0 ? ex : 0,
                               &off, s_red, s_scr, kRollTileScr, g0);
+            GSM_ACC(late_params(), wid, 6, tp5);   // emission
             if (tid == 0) {
                 KernargParams &q = late_params();
                 int64_t *const eptr = q.ro.eptr + (kSlots ? (k - 1) * q.ro.ep_s : 0);
@@ -1036,13 +1052,16 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             }
         }
         if (k < K) {
+            GSM_TNOW(tp6);
             __syncthreads();   // s_prev and the staged words read
             for (int e = tid; e < E; e += kTileBlock) s_prev[e] = s_pos[e];
             prev_edges = edges;
             arow = arow + 1 == n_act ? 0 : arow + 1;
             __syncthreads();
+            GSM_ACC(late_params(), wid, 7, tp6);   // hand-over to the next step
         }
     }
+    GSM_RSTAMP(p, b * kTileWaves + (tid >> 6), 9);
     // the final state (what the next launch or an eager step reads)
     for (int e = tid; e < E; e += kTileBlock) p.pos[eb * E + e] = s_pos[e];
     for (int w = tid; w < M * W; w += kTileBlock) p.row_mask[eb * M * W + w] = s_rm[((K - 1) & 1) * M * W + w];

@@ -1,0 +1,66 @@
+"""Timeline of one segmented rollout launch at H (navigation, 24 agents x 8192
+envs; diagnostic -DGSM_STAMPS build, run with GSM_LIB_PATH pointing at it):
+per wave, s_memrealtime (100 MHz) at the marks of gsm_roll_seg_kernel —
+0 entry, 1 state loaded, 2 step 0 physics, 3 step 0 sweep, 4 step K-1
+published, 5 tail start, 6 tail offset known (look-back), 7 tail emitted,
+8 final state stored. Prints, per mark, the percentiles over waves of the time
+since the first wave's entry, for an eager env.step (a K = 1 launch) and for a
+K-step graph replay (K = ROLL_K, default 20).
+
+Usage: GSM_LIB_PATH=.../ablate/stamps.so python tools/stamps_h_timeline.py"""
+import ctypes as C
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "gs-marl_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from gsmarl_amd import EnvConfig, GpuBatchEnv  # noqa: E402
+
+B, N, T = 8192, 24, 100
+K = int(os.environ.get("ROLL_K", 20))
+dev = "cuda:0"
+env = GpuBatchEnv(EnvConfig(scenario="navigation", n_agents=N, n_envs=B, seed=5, episode_length=T), dev)
+st = torch.zeros(B, 16, dtype=torch.int64, device=dev)
+env.lib.gsm_debug_set_stamps(env._h, C.c_void_p(st.data_ptr()))
+acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=dev)
+env.reset(seed=5, sync_edges=False)
+MARKS = ["entry", "loaded", "physics0", "sweep0", "published_last", "tail", "tail_offset", "tail_emitted", "stored"]
+
+
+def timeline():
+    q = st.cpu().numpy().astype(np.int64)
+    t0 = q[:, 0].min()
+    out = {}
+    for i, n in enumerate(MARKS):
+        v = (q[:, i] - t0) / 100.0
+        out[n] = {p: round(float(np.percentile(v, p)), 2) for p in (0, 50, 99, 100)}
+    return out
+
+
+res = {}
+for _ in range(5):
+    env.step(acts[0], sync_edges=False)
+torch.cuda.synchronize()
+st.zero_()
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+e0.record()
+env.step(acts[0], sync_edges=False)
+e1.record()
+torch.cuda.synchronize()
+res["eager_step"] = {"events_us": e0.elapsed_time(e1) * 1e3, "marks_us": timeline()}
+env.capture(acts, K, slot=0, kernels="roll")
+for _ in range(3):
+    env.replay(0)
+torch.cuda.synchronize()
+st.zero_()
+e0.record()
+env.replay(0)
+e1.record()
+torch.cuda.synchronize()
+res[f"replay_K{K}"] = {"events_us": e0.elapsed_time(e1) * 1e3, "marks_us": timeline()}
+print(json.dumps(res, indent=1))
+env.close()
