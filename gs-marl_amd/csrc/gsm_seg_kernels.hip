@@ -1602,6 +1602,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     int *s_pre = s_bc + 2 * kWavesPerBlock * kPackG;                          // [2][16]: their exclusive prefix
     int *s_red = s_pre + 2 * kWavesPerBlock * kPackG;                         // [2]: the workgroup's offset
     const int ent = m < N ? m : N + m;                                       // this lane's collider entity
+    const int wid = blockIdx.x * kWavesPerBlock + wave;                     // (diagnostic stamps)
+    (void)wid;
 
     // ---- the state before step t_first
     const float2 *pos_g = p.pos + eb * E;
@@ -1702,6 +1704,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     auto emit_prev = [&](const int k) {
         const int par = k & 1;
         const int *cb = s_bc + (1 - par) * kWavesPerBlock * kPackG;
+        GSM_TNOW(te0);
         if (wave == 0) {
             KernargParams &qe = late_params();
             const int64_t kb = (int64_t)(k - 1) * gridDim.x;
@@ -1717,7 +1720,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
         }
+        GSM_ACC(late_params(), wid, 2, te0);   // diagnostic builds: look-back (wave 0)
+        GSM_TNOW(te1);
         __syncthreads();
+        GSM_ACC(late_params(), wid, 3, te1);   // waiting for it
+        GSM_TNOW(te2);
         int64_t env_off = (int64_t)s_red[0] + s_pre[(1 - par) * kWavesPerBlock * kPackG + slot];
         const int my_cnt = cb[slot];
         if (env_off < 0) {   // a broken hand-off: never write out of bounds
@@ -1767,9 +1774,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             for (uint32_t w = row_prev & ~amask; w; w &= w - 1u) put(o++, N + __builtin_ctz(w));
         }
         wave_sync();
+        GSM_ACC(late_params(), wid, 4, te2);   // emission
     };
 
+    GSM_RSTAMP(p, wid, 8);
     for (int k = 0; k < K; ++k) {
+        GSM_TNOW(tc0);
         const int nrow = arow + 1 == n_act ? 0 : arow + 1;
         const float4 anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, agent ? m : 0);
         const float2 *const s_cur = pos_buf(k);
@@ -1873,7 +1883,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         // publish the workgroup's edge sum of this step
         const int par = k & 1;
         if (m == 0) s_bc[par * kWavesPerBlock * kPackG + slot] = env_live ? edges : 0;
+        GSM_ACC(late_params(), wid, 0, tc0);   // the step's work
+        GSM_TNOW(tc1);
         __syncthreads();
+        GSM_ACC(late_params(), wid, 1, tc1);   // the publish barrier
         if (threadIdx.x == 0) {
             int sum = 0;
             for (int j = 0; j < kWavesPerBlock * kPackG; ++j) {
@@ -1895,6 +1908,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         wave_sync();
     }
     emit_prev(K);   // the tail: the last step's edges
+    GSM_RSTAMP(p, wid, 9);
     // the final state (what the next launch or an eager step reads)
     KernargParams &q = late_params();
     const float2 *const s_fin = pos_buf(K);

@@ -11,6 +11,8 @@
 #   bash tools/gpu.sh ab TAG variant ...           same-box A/B: bench lines h / driver / c4 of the library
 #        and of lib/ablate/VARIANT.so builds (tools/build_variant.sh), alternated twice
 #   bash tools/gpu.sh envsweep TAG LINE VAR v1 v2 ...   one bench line under VAR=v (e.g. GSM_ROLL_DEPTH)
+#   bash tools/gpu.sh stamps TAG which ...         phase stamps of the lib/ablate/stamps.so build
+#        which: h (launch timeline) c2 c3 c4 (tools/stamps_*.py)
 # Outputs under gpurun_out/TAG/ (copy what is judged into profiles/).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
@@ -123,6 +125,12 @@ case $CMD in
     for v in "$@"; do
       env $var=$v timeout -k 10 300 python3 bench.py $a --no-cpu-baseline > $O/${l}_$v.json 2> $O/${l}_$v.err || { tail -20 $O/${l}_$v.err; exit 4; }
       show "$var=$v" $O/${l}_$v.json
+    done ;;
+  stamps)
+    for w in "$@"; do
+      case $w in h) sc=tools/stamps_h_timeline.py ;; c2|c3|c4) sc=tools/stamps_${w}_roll.py ;; *) echo "unknown stamps $w"; exit 9 ;; esac
+      GSM_LIB_PATH=gs-marl_amd/gsmarl_amd/lib/ablate/stamps.so timeout -k 10 200 python3 $sc > $O/stamps_$w.json 2> $O/stamps_$w.err || { tail -20 $O/stamps_$w.err; exit 7; }
+      cat $O/stamps_$w.json
     done ;;
   *) echo "unknown command $CMD"; exit 9 ;;
 esac
