@@ -376,15 +376,16 @@ int redirect(gsm_handle *h, gsm::DevParams *p, const gsm_outputs *o) {
 uint32_t next_launch_epoch();
 hipError_t clear_status(gsm_handle *h);
 
-// gsm_step as ONE launch: the config's fused rollout kernel with K = 1 (the
-// step, then its edges at the CSR offset of the in-launch look-back) instead
-// of the step kernel + the emit kernel — the same operations, so the same
-// outputs (tests/test_gpu_roll.py compares the rollout with the two-kernel
-// chain step for step). Segmented configs with a compiled rollout shape and
-// the tile path, when the grid fits one residency round (decided once per
-// handle). The ragged path keeps its two launches (a rollout launch there
-// runs the SIMD placement and the per-env slabs, built for long launches).
-// GSM_EAGER_TWO_KERNELS=1 selects the two launches everywhere.
+// gsm_step as ONE launch (opt-in, GSM_EAGER_ONE_LAUNCH=1): the config's fused
+// rollout kernel with K = 1 (the step, then its edges at the CSR offset of the
+// in-launch look-back) instead of the step kernel + the emit kernel — the same
+// operations, so the same outputs (tests/test_gpu_roll.py). Segmented configs
+// with a compiled rollout shape and the tile path, when the grid fits one
+// residency round (decided once per handle); the ragged path keeps its two
+// launches. Not the default: measured slower at H, 28.6 vs 18.7 us per step
+// (DESIGN.md §4): in one launch every wave runs the same phase at once, and the
+// last workgroup's look-back waits for the slowest of all the others' steps
+// (profiles/r4_stamps/stamps_h.json).
 constexpr int kEagerIneligible = 1;
 int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
     if (h->eager_roll == 0 || p.path == gsm::kPathRagged) return kEagerIneligible;
@@ -401,7 +402,8 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
     const size_t lds = tile ? gsm::roll_tile_kernel_lds(p) : gsm::roll_kernel_lds(p);
     if (h->eager_roll < 0) {
         h->eager_roll = 0;
-        if (const char *ev = getenv("GSM_EAGER_TWO_KERNELS")) if (atoi(ev) != 0) return kEagerIneligible;
+        const char *ev = getenv("GSM_EAGER_ONE_LAUNCH");
+        if (!ev || atoi(ev) == 0) return kEagerIneligible;
         int dev = 0, per_cu = 0, n_cu = 0;
         hipError_t e = hipGetDevice(&dev);
         if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);

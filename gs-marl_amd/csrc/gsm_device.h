@@ -385,26 +385,21 @@ __device__ __forceinline__ void xfer_grp_publish(const Xfer &x, uint64_t l, int 
 // of those in between), otherwise the window's aggregates are added and the
 // walk moves on. Aggregates were published an iteration earlier, so the walk
 // never waits on an inclusive prefix; an aggregate read early is re-polled.
-// A walk that finds no inclusive prefix in its first window (workgroups in
-// lockstep: a launch's first and last steps) reads the remaining windows
-// kLookbackTail at a time, all loads issued before the first is used: one load
-// latency per batch instead of one per window. (Batching every round, the
-// first included, was measured slower at H: 10.2 vs 9.8 us per step.)
-#ifndef GSM_LOOKBACK_TAIL   // A/B (temporary)
-#define GSM_LOOKBACK_TAIL 1
-#endif
-constexpr int kLookbackTail = GSM_LOOKBACK_TAIL;
+// (Reading several windows per round before using the first, so a long walk
+// pays one load latency per round, was measured slower at H — four windows
+// every round: 10.2 vs 9.8 us per step; eight per round after a first single
+// window: 8.6 vs 8.4 — and for the one-launch eager step)
 __device__ __forceinline__ int roll_lookback(const uint64_t *agg_k, const uint64_t *inc_k, uint32_t tag,
                                              uint32_t *status, int lane) {
     int acc = 0;
     int first = (int)blockIdx.x;
     asm volatile("" : "+s"(first));   // no window predicates hoisted into a rollout's loop (SGPR pairs)
-    // one window [hi - 64, hi) from loaded inclusive / aggregate words; true
-    // when the walk ends there
-    auto window = [&](int hi, uint64_t xi, uint64_t a) {
+    for (int hi = first; hi > 0; hi -= kWave) {
         const int idx = hi - 1 - lane;                      // lane 0 = nearest predecessor
         const int ci = idx >= 0 ? idx : 0;
         const bool valid = idx >= 0;
+        const uint64_t xi = __hip_atomic_load((const gu64 *)(inc_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t a = __hip_atomic_load((const gu64 *)(agg_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t have = __ballot(valid && (uint32_t)(xi >> 32) == tag);
         const int j = have ? __builtin_ctzll(have) : kWave;   // wave-uniform
         // aggregates of lanes < j (all valid lanes when no inclusive was found)
@@ -413,32 +408,9 @@ __device__ __forceinline__ int roll_lookback(const uint64_t *agg_k, const uint64
         int v = need ? (int)(uint32_t)a : 0;
         if (lane == j) v = (int)(uint32_t)xi;
         acc += wave_total(v);
-        return have != 0 || hi <= kWave;
-    };
-    auto ld = [&](const uint64_t *base, int hi) {
-        const int idx = hi - 1 - lane;
-        return __hip_atomic_load((const gu64 *)(base + (idx >= 0 ? idx : 0)), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-    };
-    int hi = first;
-    if (hi <= 0) return 0;
-    if constexpr (kLookbackTail == 1) {
-        for (;; hi -= kWave)
-            if (window(hi, ld(inc_k, hi), ld(agg_k, hi))) return acc;
-    } else {
-        if (window(hi, ld(inc_k, hi), ld(agg_k, hi))) return acc;
-        for (hi -= kWave;; hi -= kWave * kLookbackTail) {
-            uint64_t xi[kLookbackTail], xa[kLookbackTail];
-#pragma unroll
-            for (int u = 0; u < kLookbackTail; ++u) {
-                xi[u] = ld(inc_k, hi - u * kWave);
-                xa[u] = ld(agg_k, hi - u * kWave);
-            }
-#pragma unroll
-            for (int u = 0; u < kLookbackTail; ++u)
-                if (window(hi - u * kWave, xi[u], xa[u])) return acc;
-        }
+        if (have) return acc;
     }
+    return acc;
 }
 
 }  // namespace gsm

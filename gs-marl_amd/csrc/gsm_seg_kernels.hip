@@ -1260,14 +1260,21 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         const int par = k & 1;
         const int *cb = s_bc + (1 - par) * kWavesPerBlock;   // this workgroup's counts of step t - 1
         // the env's list staged first (needs only its own row counts)
+        GSM_TNOW(te0);
         const int staged = wave_live ? stage_rows<kN, kNo>(L, (uint32_t *)s_nf, scr_cap, oo) : -1;
+        GSM_ACC(p, L.b, 14, te0);   // diagnostic builds: staging (emission, below, adds to it)
+        GSM_TNOW(te1);
         // wave 0 walks back over the predecessors, hands the workgroup's
         // offset to the other waves and publishes its inclusive prefix
         if (wave == 0) {
             KernargParams &qe = late_params();
             const int64_t kb = (int64_t)(k - 1) * gridDim.x;
+#if GSM_ABL_HANDOFF   // ablation builds only (wrong offsets): the step without the look-back
+            const int ex = 0;
+#else
             const int ex = roll_lookback(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
                                          etag | (uint32_t)k, qe.roll.status, L.lane);
+#endif
             if (L.lane == 0) {
                 s_red[0] = ex;
                 __hip_atomic_store((gu64 *)(qe.roll.gran + (int64_t)K * gridDim.x + kb + blockIdx.x),
@@ -1276,7 +1283,13 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
+        GSM_ACC(p, L.b, 12, te1);   // look-back (wave 0)
+        GSM_TNOW(te2);
+#if GSM_ABL_HANDOFF < 2
         __syncthreads();
+#endif
+        GSM_ACC(p, L.b, 13, te2);   // waiting for it
+        GSM_TNOW(te3);
         if (k == K) GSM_RSTAMP(p, L.b, 6);
         // (the prefix formed once by thread 0, not w < wave selects: those
         // are loop-invariant lane masks the compiler holds in SGPR pairs)
@@ -1305,6 +1318,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
                 emit_rows<kN, kNo, 1>(s, L, s_prev, oo, env_off, out, env_off + my_cnt > out.cap);
         }
         wave_sync();
+        GSM_ACC(p, L.b, 14, te3);
     };
     for (int k = 0; k < K; ++k) {
         // lane-derived values re-formed every iteration (an asm barrier): held
@@ -1312,6 +1326,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         Lane L = L0;
         asm volatile("" : "+v"(L.lane), "+v"(L.m));
         const int m = L.m;
+        GSM_TNOW(tw0);
         const uint32_t um = (uint32_t)m, ma = L.lane < N ? (uint32_t)L.lane : N - 1;
         // the next step's actions, in flight during this step
         const int nrow = arow + 1 == n_act ? 0 : arow + 1;
@@ -1460,7 +1475,12 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         // publish the workgroup's edge sum of step t
         const int par = k & 1;
         if (L.lane == 0) s_bc[par * kWavesPerBlock + wave] = wave_edges;
+        GSM_ACC(p, L.b, 10, tw0);   // the step's work
+        GSM_TNOW(tw1);
+#if GSM_ABL_HANDOFF < 2
         __syncthreads();
+#endif
+        GSM_ACC(p, L.b, 11, tw1);   // the publish barrier
         if (threadIdx.x == 0) {
             int sum = 0;
             for (int w = 0; w < kWavesPerBlock; ++w) {
