@@ -1301,7 +1301,7 @@ __device__ __forceinline__ uint64_t place_ld(const uint64_t *g) {   // a wave-un
            __builtin_amdgcn_readfirstlane((uint32_t)x);
 }
 __device__ __forceinline__ uint64_t *place_area(const KernargParams &q) {
-    return q.roll.gran + 2 + (int64_t)q.roll.K * (q.roll.xW + q.roll.xNG);
+    return q.roll.gran + (int64_t)q.roll.K * (q.roll.xW + q.roll.xNG);   // (roll.gran is past the header)
 }
 // Registration counters are spread over kGroups words (XCC x shader engine)
 // so that no word takes more than ~128 atomics per launch.
@@ -1497,7 +1497,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         Xfer x;
         x.W = q.roll.xW;
         x.NG = q.roll.xNG;
-        x.agg = q.roll.gran + 2;
+        x.agg = q.roll.gran;   // (past the allocation's 16-byte header already)
         x.grp = x.agg + (int64_t)q.roll.K * x.W;
         x.status = q.roll.status;
         x.etag = roll_epoch_tag(epoch);

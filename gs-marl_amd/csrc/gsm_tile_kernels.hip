@@ -851,6 +851,33 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         uint64_t *const rout = s_rm + (k & 1) * M * W;
         const uint64_t *const rkeep = s_rm + ((k + 1) & 1) * M * W;   // the previous step's masks
         int edges = 0;
+        // the previous step's CSR offset: the look-back by the last wave, idle
+        // in the physics below (agents 0..N-1 on the first threads), so its
+        // latency overlaps the step; read by the emission after the step
+        // (s_x[2], published by the step's barriers)
+        if (k > 0 && wave == kTileWaves - 1) {
+            GSM_TNOW(tp4);
+            const int64_t kb = (int64_t)(k - 1) * gridDim.x;
+            KernargParams &q = late_params();
+            int ex = roll_lookback(q.roll.gran + kb, q.roll.gran + (int64_t)K * gridDim.x + kb, etag | (uint32_t)k,
+                                   q.roll.status, lane);
+            if (lane == 0) {
+                __hip_atomic_store((gu64 *)(late_params().roll.gran + (int64_t)K * gridDim.x + kb + b),
+                                   ((uint64_t)(etag | (uint32_t)k) << 32) | (uint32_t)(ex + prev_edges),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                // (an offset past the capacity is a legal overflow of a small
+                // slot: edge_ptr keeps it, emit_env stops its writes at the
+                // capacity)
+                if (ex < 0) {   // a broken hand-off: never write out of bounds
+                    __hip_atomic_store((gu32 *)late_params().roll.status, 2u, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    ex = (int)min(late_params().ro.cap, (int64_t)0x7fffffff);
+                }
+                s_x[2] = ex;
+            }
+            GSM_ACC(late_params(), wid, 5, tp4);   // look-back (last wave)
+        }
+        if (k == K) __syncthreads();   // (the tail: no step; s_x[2] for the emission)
         if (k < K) {
         bool relaid = false;
         auto relayout = [&]() {   // scenario.reset_world with the Philox layout
@@ -1018,31 +1045,10 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         }   // k < K
         // the previous step's edges at the offset of the look-back
         if (k > 0) {
-            int ex = 0;
-            GSM_TNOW(tp4);
-            if (wave == 0) {
-                const int64_t kb = (int64_t)(k - 1) * gridDim.x;
-                KernargParams &q = late_params();
-                ex = roll_lookback(q.roll.gran + kb, q.roll.gran + (int64_t)K * gridDim.x + kb, etag | (uint32_t)k,
-                                   q.roll.status, lane);
-                if (lane == 0) {
-                    __hip_atomic_store((gu64 *)(late_params().roll.gran + (int64_t)K * gridDim.x + kb + b),
-                                       ((uint64_t)(etag | (uint32_t)k) << 32) | (uint32_t)(ex + prev_edges),
-                                       __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            // (an offset past the capacity is a legal overflow of a small slot:
-            // edge_ptr keeps it, emit_env stops its writes at the capacity)
-            if (ex < 0) {   // a broken hand-off: never write out of bounds
-                __hip_atomic_store((gu32 *)late_params().roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                ex = (int)min(late_params().ro.cap, (int64_t)0x7fffffff);
-            }
-            GSM_ACC(late_params(), wid, 5, tp4);   // look-back (wave 0)
             GSM_TNOW(tp5);
             int64_t off;
-            emit_env<kN, kNo>(p, roll_edge_sink<kSlots>(late_params(), k - 1, K), s_prev, rkeep, tid == 0 ? ex : 0,
-                              &off, s_red, s_scr, kRollTileScr, g0);
+            emit_env<kN, kNo>(p, roll_edge_sink<kSlots>(late_params(), k - 1, K), s_prev, rkeep,
+                              tid == 0 ? s_x[2] : 0, &off, s_red, s_scr, kRollTileScr, g0);
             GSM_ACC(late_params(), wid, 6, tp5);   // emission
             if (tid == 0) {
                 KernargParams &q = late_params();
