@@ -410,7 +410,10 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
         if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, gsm::block_threads(p), lds);
         if (e != hipSuccess) return hip_fail(h, e, "occupancy query (eager rollout)");
         if ((int64_t)per_cu * n_cu < nb) return kEagerIneligible;
-        const size_t bytes = 16 + 2 * (size_t)nb * sizeof(uint64_t);
+        // (look-back: aggregates + inclusive prefixes per workgroup; packed
+        // small envs: per-wave counts + group sums)
+        const size_t xw = (size_t)nb * gsm::kWavesPerBlock;
+        const size_t bytes = 16 + std::max(2 * (size_t)nb, xw + (xw + gsm::kWave - 1) / gsm::kWave) * sizeof(uint64_t);
         e = hipMalloc(&h->eager_gran, bytes);
         if (e != hipSuccess) { h->eager_gran = nullptr; return hip_fail(h, e, "hipMalloc (eager granules)"); }
         e = gsm::launch_granule_init(h->eager_gran, bytes, 0u, nullptr);
@@ -426,7 +429,8 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
     // the step's outputs: the bound (or redirected) buffers, its edges too
     p.ro = gsm::DevParams::RollOut{p.node_feat, p.reward, p.cost, p.done, p.edge_count, p.edge_ptr, p.edge_index,
                                    p.edge_attr, 0, 0, 0, 0, 0, 0, 0, p.edge_capacity, nullptr, nullptr, p.assign, 0};
-    p.roll = gsm::DevParams::Roll{(const char *)p.actions, 0, 1, 0, 1, 0, 0, 0, 0, 0, h->eager_gran + 2,
+    const int xW = nb * gsm::kWavesPerBlock, xNG = (xW + gsm::kWave - 1) / gsm::kWave;
+    p.roll = gsm::DevParams::Roll{(const char *)p.actions, 0, 1, 0, 1, xW, xNG, 0, 0, 0, h->eager_gran + 2,
                                   h->roll_status, next_launch_epoch(), 0, nullptr, nullptr, 0, 0};
     void *args[] = {&p};
     const hipError_t e = hipLaunchKernel(fn, dim3(nb), dim3(gsm::block_threads(p)), args, (unsigned)lds, s);
@@ -783,10 +787,12 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         if (fallback) return kRollIneligible;
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: n_steps must be <= 4094");
     }
-    // ragged: per-wave granules, groups of 64 waves (at most 128 groups: one
-    // residency round holds <= 8192 waves), edges packed `depth` steps late
+    // ragged and packed small envs: per-wave granules, groups of 64 waves (at
+    // most 128 groups: one residency round holds <= 8192 waves); ragged: edges
+    // packed `depth` steps late
     const int xW = nb * gsm::kWavesPerBlock, xNG = (xW + gsm::kWave - 1) / gsm::kWave;
-    if (ragged && xNG > 2 * gsm::kWave) {
+    const bool per_wave = ragged || (!tile && gsm::roll_packed(p));   // per-wave granules (Xfer)
+    if (per_wave && xNG > 2 * gsm::kWave) {
         if (fallback) return kRollIneligible;
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: more than 8192 envs in one rollout launch");
     }
@@ -841,13 +847,13 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     }
     gsm_handle::Slot &sl = h->slots[slot];
     drop_slot(sl);
-    // a 16-byte header (unused), then 8-byte granules. Ragged:
-    // per-wave counts [K][xW] and group sums [K][xNG]; segmented / tile:
+    // a 16-byte header (unused), then 8-byte granules. Ragged and packed
+    // small envs: per-wave counts [K][xW] and group sums [K][xNG]; segmented / tile:
     // aggregates [K][nb] and inclusive prefixes [K][nb] (look-back). Zeroed
     // once here — granules are tagged with the launch epoch, so replays never
     // clear them
     // (ragged: then the placement words, gsm::PlaceArea)
-    const size_t gran_alloc = 16 + (size_t)K * (ragged ? (size_t)(xW + xNG) : 2 * (size_t)nb) * sizeof(uint64_t) +
+    const size_t gran_alloc = 16 + (size_t)K * (per_wave ? (size_t)(xW + xNG) : 2 * (size_t)nb) * sizeof(uint64_t) +
                               (ragged ? gsm::PlaceArea::words(xW) * sizeof(uint64_t) : 0);
     e = hipMalloc(&sl.gran, gran_alloc);
     if (e != hipSuccess) {

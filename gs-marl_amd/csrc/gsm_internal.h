@@ -108,7 +108,7 @@ struct DevParams {
         const char *actions;
         int64_t stride;
         int32_t n_actions, t_first, K;
-        int32_t xW, xNG;      // per-wave hand-off (ragged rollout): waves of the grid, groups of 64 (gsm_device.h Xfer)
+        int32_t xW, xNG;      // per-wave hand-off (ragged and packed rollouts): waves of the grid, groups of 64 (gsm_device.h Xfer)
         int32_t depth;        // ragged rollout: steps between an env's step and the packing of its edges
         int32_t slab_e;       // ragged rollout: edges per env slab (the config's max_edges_per_env)
         int32_t place_R;      // ragged rollout placement: waves per SIMD when the grid fills every SIMD
@@ -178,7 +178,10 @@ const void *emit_seg_kernel_fn(const DevParams &p);
 // fused K-step rollout kernel (nullptr where the config has none: G > 1,
 // runtime shapes, other families) and its LDS bytes
 const void *roll_seg_kernel_fn(const DevParams &p, bool slots);   // slots: a rollout buffer's outputs
-int roll_seg_envs_per_block(const DevParams &p);   // 4 (one env per wave) or 16 (small envs, four per wave)
+int roll_seg_envs_per_block(const DevParams &p);
+// the segmented rollout packs four small envs per wave (gsm_roll_pack_kernel):
+// per-wave CSR hand-off granules, as the ragged rollout (Roll::xW / xNG)
+bool roll_packed(const DevParams &p);   // 4 (one env per wave) or 16 (small envs, four per wave)
 size_t roll_kernel_lds(const DevParams &p);
 const void *roll_tile_kernel_fn(const DevParams &p, bool slots);   // nullptr unless p.tile_sym
 size_t roll_tile_kernel_lds(const DevParams &p);

@@ -1572,7 +1572,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
 // step's workgroup sums are the config's block_edge_sum directly).
 constexpr int kPackSeg = 16, kPackG = kWave / kPackSeg;   // lanes per env, envs per wave
 template <int kN, int kNo>
-constexpr int pack_lds_wave() { return 2 * 8 * kPackG * (2 * kN + kNo) + 8 * kPackG * kN; }
+constexpr int pack_lds_wave() { return 3 * 8 * kPackG * (2 * kN + kNo) + 8 * kPackG * kN; }
 template <int kCtrl>
 __device__ __forceinline__ int dpp_row0(int v) {   // DPP within 16-lane rows, 0 shifted in
     return __builtin_amdgcn_update_dpp(0, v, kCtrl, 0xf, 0xf, true);
@@ -1612,15 +1612,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const bool env_live = b < p.B;
     const bool live = env_live && m < M, agent = live && m < N;
     const int64_t eb = env_live ? b : 0;
-    // LDS per wave: positions ping-pong [2][G][E] (step k reads buffer k & 1,
-    // its agents' new positions go to the other; goals and obstacles kept in
-    // both), the next step's forces [G][N]
+    // LDS per wave: positions [3][G][E] in rotation — buffer `cur` holds the
+    // positions before step k, step k writes all of its env's rows into the
+    // next (agents integrated, goals / obstacles carried or relaid), and the
+    // one before `cur` still holds the positions after step k - 2, whose
+    // edges this iteration emits — then the next step's forces [G][N]
     float2 *const s_w = (float2 *)(smem + wave * pack_lds_wave<kN, kNo>());
-    auto pos_buf = [&](int k) { return s_w + (k & 1) * kPackG * E + seg * E; };   // this env's rows
-    float2 *const s_force = s_w + 2 * kPackG * E + seg * N;
-    int *s_bc = (int *)(smem + kWavesPerBlock * pack_lds_wave<kN, kNo>());   // [2][16]: env counts by parity
-    int *s_pre = s_bc + 2 * kWavesPerBlock * kPackG;                          // [2][16]: their exclusive prefix
-    int *s_red = s_pre + 2 * kWavesPerBlock * kPackG;                         // [2]: the workgroup's offset
+    auto pos_buf = [&](int i) { return s_w + i * kPackG * E + seg * E; };   // this env's rows in buffer i
+    float2 *const s_force = s_w + 3 * kPackG * E + seg * N;
+    int *s_bc = (int *)(smem + kWavesPerBlock * pack_lds_wave<kN, kNo>());   // [waves]: the last step's counts
     const int ent = m < N ? m : N + m;                                       // this lane's collider entity
     const int wid = blockIdx.x * kWavesPerBlock + wave;                     // (diagnostic stamps)
     (void)wid;
@@ -1633,7 +1633,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     float2 acc = env_live ? p.ep_acc[eb] : make_float2(0.0f, 0.0f);
     uint32_t cand_prev = agent ? (uint32_t)p.contact_mask[eb * N + m] : 0u;
     const float4 a0 = roll_action_load<kN, kFmt>(p, p.roll.t_first % p.roll.n_actions, eb, agent ? m : 0);
-    if (env_live && m < E) pos_buf(0)[m] = pos_buf(1)[m] = x;
+    if (env_live && m < E) pos_buf(0)[m] = x;
     wave_sync();
 
     // one pass over the env's M columns from the positions at `s` (lane m:
@@ -1712,59 +1712,63 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     }
 
     const int K = p.roll.K, n_act = p.roll.n_actions;
-    const uint32_t etag = roll_epoch_tag(p.roll.epoch);
     int arow = p.roll.t_first % n_act;
-    uint32_t row_prev = 0;       // the previous step's radius row bits (emitted one iteration on)
+    // CSR hand-off per wave (gsm_device.h Xfer: each wave publishes its four
+    // envs' edge count of step k in iteration k, the last wave of each group
+    // of 64 their group sum in iteration k + 1, and step k's edges are written
+    // in iteration k + 2 at the offset those give) — no workgroup barrier and
+    // no look-back walk in the loop: every granule a wave reads was published
+    // an iteration before, and its loads are issued before the step's work
+    const int w = blockIdx.x * kWavesPerBlock + wave;      // this wave's index in the grid
+    const bool glast = (w & 63) == 63;                      // publishes its group's sums
+    auto xf = [&]() -> Xfer {
+        KernargParams &q = late_params();
+        Xfer x;
+        x.W = q.roll.xW;
+        x.NG = q.roll.xNG;
+        x.agg = q.roll.gran;
+        x.grp = x.agg + (int64_t)q.roll.K * x.W;
+        x.status = q.roll.status;
+        x.etag = roll_epoch_tag(q.roll.epoch);
+        return x;
+    };
+    uint32_t row_m1 = 0, row_m2 = 0;   // radius row bits of steps k - 1 and k - 2
+    int cnt_m1 = 0;                    // this wave's edge count of step k - 1
     uint32_t cand_keep = cand_prev;
     bool coinc = false;
-    const int slot = wave * kPackG + seg;   // this env's index in the workgroup
+    int cur = 0;                       // the buffer holding the positions before step k
+    auto next_buf = [](int i) { return i == 2 ? 0 : i + 1; };
+    auto prev_buf = [](int i) { return i == 0 ? 2 : i - 1; };
 
-    // the edges of the step before iteration k (positions pos_buf(k), rows
-    // row_prev) at the offset of the look-back (every wave of the workgroup)
-    auto emit_prev = [&](const int k) {
-        const int par = k & 1;
-        const int *cb = s_bc + (1 - par) * kWavesPerBlock * kPackG;
-        GSM_TNOW(te0);
-        if (wave == 0) {
-            KernargParams &qe = late_params();
-            const int64_t kb = (int64_t)(k - 1) * gridDim.x;
-            const int ex = roll_lookback(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
-                                         etag | (uint32_t)k, qe.roll.status, lane);
-            if (lane == 0) {
-                int tot = 0;
-#pragma unroll
-                for (int j = 0; j < kWavesPerBlock * kPackG; ++j) tot += cb[j];
-                s_red[0] = ex;
-                __hip_atomic_store((gu64 *)(qe.roll.gran + (int64_t)K * gridDim.x + kb + blockIdx.x),
-                                   ((uint64_t)(etag | (uint32_t)k) << 32) | (uint32_t)(ex + tot), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-            }
-        }
-        GSM_ACC(late_params(), wid, 2, te0);   // diagnostic builds: look-back (wave 0)
-        GSM_TNOW(te1);
-        __syncthreads();
-        GSM_ACC(late_params(), wid, 3, te1);   // waiting for it
+    // the edges of step j (positions in buffer `pb`, rows `row`) at the wave's
+    // offset `woff`: each env after the wave's earlier envs
+    auto emit = [&](const int j, const int pb, const uint32_t row, const int woff) {
         GSM_TNOW(te2);
-        int64_t env_off = (int64_t)s_red[0] + s_pre[(1 - par) * kWavesPerBlock * kPackG + slot];
-        const int my_cnt = cb[slot];
-        if (env_off < 0) {   // a broken hand-off: never write out of bounds
-            if (lane == 0)
-                __hip_atomic_store((gu32 *)late_params().roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            env_off = late_params().ro.cap;
-        }
         KernargParams &qs = late_params();
-        if (env_live && m == 0) {
-            int64_t *const eptr = qs.ro.eptr + (kSlots ? (k - 1) * qs.ro.ep_s : 0);
-            eptr[b] = env_off;
-            if (b == qs.B - 1) eptr[qs.B] = env_off + my_cnt;
-        }
         // rows in entity order: agent rows (agent columns, own goal, obstacle
         // columns), goal rows, obstacle rows (agent then obstacle columns)
-        const int c = live ? __popc(row_prev) + (agent ? 1 : 0) : 0;
+        const int c = live ? __popc(row) + (agent ? 1 : 0) : 0;
         const int incl = seg_scan16(c);
         const int a_total = seg_sum16(agent ? c : 0);
-        const EdgeSink out = roll_edge_sink<kSlots>(qs, k - 1, K);
-        const float2 *sp = pos_buf(k);
+        // env totals (segment sums plus the N goal rows) and the wave's
+        // exclusive prefix over its envs
+        const int e_tot = env_live ? seg_sum16(c) + N : 0;
+        const int t0 = __builtin_amdgcn_readlane(e_tot, 0), t1 = __builtin_amdgcn_readlane(e_tot, 16),
+                  t2 = __builtin_amdgcn_readlane(e_tot, 32);
+        const int before = (seg > 0 ? t0 : 0) + (seg > 1 ? t1 : 0) + (seg > 2 ? t2 : 0);
+        int64_t env_off = (int64_t)woff + before;
+        if (woff < 0) {   // a broken hand-off: never write out of bounds
+            if (lane == 0)
+                __hip_atomic_store((gu32 *)qs.roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            env_off = qs.ro.cap;
+        }
+        if (env_live && m == 0) {
+            int64_t *const eptr = qs.ro.eptr + (kSlots ? j * qs.ro.ep_s : 0);
+            eptr[b] = env_off;
+            if (b == qs.B - 1) eptr[qs.B] = env_off + e_tot;
+        }
+        const EdgeSink out = roll_edge_sink<kSlots>(qs, j, K);
+        const float2 *sp = pos_buf(pb);
         const int32_t g0 = (int32_t)(eb * E);
         if (live) {
             int64_t o = env_off + (incl - c) + (m >= N ? N : 0);
@@ -1779,7 +1783,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                 }
             };
             constexpr uint32_t amask = (1u << N) - 1u;
-            for (uint32_t w = row_prev & amask; w; w &= w - 1u) put(o++, __builtin_ctz(w));
+            for (uint32_t bits = row & amask; bits; bits &= bits - 1u) put(o++, __builtin_ctz(bits));
             if (agent) {
                 put(o++, N + m);                                     // agent m -> its goal
                 const float2 g = sp[N + m];
@@ -1791,21 +1795,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                     out.attr[at] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
                 }
             }
-            for (uint32_t w = row_prev & ~amask; w; w &= w - 1u) put(o++, N + __builtin_ctz(w));
+            for (uint32_t bits = row & ~amask; bits; bits &= bits - 1u) put(o++, N + __builtin_ctz(bits));
         }
-        wave_sync();
-        GSM_ACC(late_params(), wid, 4, te2);   // emission
+        GSM_ACC(late_params(), wid, 4, te2);   // diagnostic builds: emission
     };
 
     GSM_RSTAMP(p, wid, 8);
     for (int k = 0; k < K; ++k) {
+        // the hand-off loads of this iteration, in flight during the step
+        XferOff xo{0ull, 0ull, 0ull};
+        uint64_t gl = 0;
+        if (k >= 2) xo = xfer_off_load(xf(), k - 2, w, lane);
+        if (k >= 1 && glast) gl = xfer_grp_load(xf(), k - 1, w, lane);
         GSM_TNOW(tc0);
         const int nrow = arow + 1 == n_act ? 0 : arow + 1;
         const float4 anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, agent ? m : 0);
-        const float2 *const s_cur = pos_buf(k);
-        float2 *const s_pos = pos_buf(k + 1);
+        const float2 *const s_cur = pos_buf(cur);
+        float2 *const s_pos = pos_buf(next_buf(cur));
         KernargParams &pc = late_params();
-        // apply_environment_force (formed by the previous sweep) + integrate_state
+        // apply_environment_force (formed by the previous sweep) + integrate_state;
+        // goals and obstacles carried into the step's buffer
         if (agent) {
             const float2 pi = s_cur[m];
             const float2 F0 = s_force[m];
@@ -1827,6 +1836,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                 }
             }
             s_pos[m] = make_float2(pi.x + v.x * dt, pi.y + v.y * dt);
+        } else if (env_live && m < E) {
+            s_pos[m] = s_cur[m];
         }
         wave_sync();
         t += 1;
@@ -1899,45 +1910,56 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             (q.ro.done + (kSlots ? k * q.ro.done_s : 0))[b] = done ? 1 : 0;
             if (kSlots || k == K - 1) (q.ro.ecount + (kSlots ? k * q.ro.ec_s : 0))[b] = edges;
         }
-
-        // publish the workgroup's edge sum of this step
-        const int par = k & 1;
-        if (m == 0) s_bc[par * kWavesPerBlock * kPackG + slot] = env_live ? edges : 0;
-        GSM_ACC(late_params(), wid, 0, tc0);   // the step's work
+        // publish the wave's count of this step, then (a group's last wave)
+        // the group sum of the previous step
+        const int ev = env_live ? edges : 0;
+        const int wcnt = __builtin_amdgcn_readlane(ev, 0) + __builtin_amdgcn_readlane(ev, 16) +
+                         __builtin_amdgcn_readlane(ev, 32) + __builtin_amdgcn_readlane(ev, 48);
+        GSM_ACC(late_params(), wid, 0, tc0);   // diagnostic builds: the step's work
         GSM_TNOW(tc1);
-        __syncthreads();
-        GSM_ACC(late_params(), wid, 1, tc1);   // the publish barrier
-        if (threadIdx.x == 0) {
-            int sum = 0;
-            for (int j = 0; j < kWavesPerBlock * kPackG; ++j) {
-                s_pre[par * kWavesPerBlock * kPackG + j] = sum;
-                sum += s_bc[par * kWavesPerBlock * kPackG + j];
-            }
-            __hip_atomic_store((gu64 *)(q.roll.gran + (int64_t)k * gridDim.x + blockIdx.x),
-                               ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)sum, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-            if (k == K - 1) q.block_edge_sum[blockIdx.x] = sum;   // the config's G = 4 workgroup layout
+        if (lane == 0) xfer_st(xf().agg + (int64_t)k * xf().W + w, xf().tag(k), (uint32_t)wcnt);
+        if (k >= 1 && glast) xfer_grp_publish(xf(), gl, k - 1, w, lane, cnt_m1);
+        GSM_ACC(late_params(), wid, 1, tc1);   // publish
+        // the edges of step k - 2 (positions in the buffer before `cur`)
+        if (k >= 2) {
+            GSM_TNOW(te0);
+            const int woff = xfer_off_settle(xf(), xo, k - 2, w, lane);
+            GSM_ACC(late_params(), wid, 3, te0);   // the offset settled
+            emit(k - 2, prev_buf(cur), row_m2, woff);
         }
-        if (k > 0) emit_prev(k);
-        row_prev = rad;
+        row_m2 = row_m1;
+        row_m1 = rad;
+        cnt_m1 = wcnt;
         cand_keep = cand;
-        if (__builtin_expect(__any(reset), 0)) {   // the new episode's statics into the other buffer
-            if (reset && m >= N && m < E) pos_buf(k)[m] = s_pos[m];
-        }
+        cur = next_buf(cur);
         arow = nrow;
         wave_sync();
     }
-    emit_prev(K);   // the tail: the last step's edges
+    // the tail: the group sums of the last step, then the edges of the last two
+    const int fin = cur;   // positions after the last step
+    for (int k = K; k < K + 2; ++k) {
+        XferOff xo{0ull, 0ull, 0ull};
+        if (k >= 2) xo = xfer_off_load(xf(), k - 2, w, lane);
+        if (k == K && K >= 1 && glast) xfer_grp_publish(xf(), xfer_grp_load(xf(), K - 1, w, lane), K - 1, w, lane, cnt_m1);
+        if (k >= 2) emit(k - 2, prev_buf(cur), row_m2, xfer_off_settle(xf(), xo, k - 2, w, lane));
+        row_m2 = row_m1;
+        cur = next_buf(cur);
+    }
     GSM_RSTAMP(p, wid, 9);
-    // the final state (what the next launch or an eager step reads)
+    // the last step's sums in the config's workgroup layout (G = 4: the same
+    // 16 envs per workgroup), for the emit launch that may follow
+    if (lane == 0) s_bc[wave] = cnt_m1;
+    __syncthreads();
     KernargParams &q = late_params();
-    const float2 *const s_fin = pos_buf(K);
+    if (threadIdx.x == 0 && K >= 1) q.block_edge_sum[blockIdx.x] = s_bc[0] + s_bc[1] + s_bc[2] + s_bc[3];
+    // the final state (what the next launch or an eager step reads)
+    const float2 *const s_fin = pos_buf(fin);
     if (env_live && m < E) q.pos[eb * E + m] = s_fin[m];
     if (agent) {
         q.vel[eb * N + m] = v;
         q.contact_mask[eb * N + m] = cand_keep;
     }
-    if (live) q.row_mask[eb * M + m] = row_prev;
+    if (live) q.row_mask[eb * M + m] = row_m1;
     if (env_live && m == 0) {
         q.step_count[b] = t;
         q.episode[b] = ep;
@@ -1977,7 +1999,7 @@ const void *lag_step_seg_kernel_fn(const DevParams &p) { return pick_step_seg<tr
 
 // small shapes run four envs per wave (gsm_roll_pack_kernel)
 #define GSM_PACK_SHAPES(X) X(3, 3)
-static bool roll_packed(const DevParams &p) {
+bool roll_packed(const DevParams &p) {
 #define GSM_PICK(n, no) if (p.N == n && p.No == no) return true;
     GSM_PACK_SHAPES(GSM_PICK)
 #undef GSM_PICK
@@ -2015,7 +2037,7 @@ const void *roll_seg_kernel_fn(const DevParams &p, bool slots) {
 }
 size_t roll_kernel_lds(const DevParams &p) {
 #define GSM_PICK(n, no) \
-    if (p.N == n && p.No == no) return (size_t)kWavesPerBlock * pack_lds_wave<n, no>() + 4 * (4 * kWavesPerBlock * kPackG + 2);
+    if (p.N == n && p.No == no) return (size_t)kWavesPerBlock * pack_lds_wave<n, no>() + 4 * kWavesPerBlock;
     GSM_PACK_SHAPES(GSM_PICK)
 #undef GSM_PICK
     return (size_t)kWavesPerBlock * roll_lds_wave(p.N, p.E) + 4 * (4 * kWavesPerBlock + 2);
