@@ -357,6 +357,19 @@ __device__ __forceinline__ XferOff xfer_off_load(const Xfer &x, int s, int w, in
     o.g1 = g > kWave ? xfer_ld(gg + min(lane + kWave, gl)) : 0ull;   // wave-uniform branch
     return o;
 }
+// The same loads with none under a branch (g1 always loaded): for a loop
+// that keeps them in flight across other loads' waits
+__device__ __forceinline__ XferOff xfer_off_load_all(const Xfer &x, int s, int w, int lane) {
+    const int g = w >> 6, r = w & 63;
+    const uint64_t *ag = x.agg + (int64_t)s * x.W + (g << 6);
+    const uint64_t *gg = x.grp + (int64_t)s * x.NG;
+    const int gl = g > 0 ? g - 1 : 0;
+    XferOff o;
+    o.a = xfer_ld(ag + min(lane, r > 0 ? r - 1 : 0));
+    o.g0 = xfer_ld(gg + min(lane, gl));
+    o.g1 = xfer_ld(gg + min(lane + kWave, gl));
+    return o;
+}
 __device__ __forceinline__ int xfer_off_settle(const Xfer &x, const XferOff &o, int s, int w, int lane) {
     const int g = w >> 6, r = w & 63, gl = g > 0 ? g - 1 : 0;
     const uint32_t tag = x.tag(s);

@@ -1645,13 +1645,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                      float2 *F) {
         KernargParams &q = late_params();
         uint32_t r2b1 = __float_as_uint(q.R2) + 1u;
-        uint32_t cutb = __float_as_uint(m < N ? q.cut2_aa : q.cut2_ao);   // this row's partner class: see below
-        asm volatile("" : "+v"(r2b1), "+v"(cutb));
+        asm volatile("" : "+v"(r2b1));
         // (the candidate threshold is the PAIR's: agent-agent for agent columns
         // of an agent row, agent-obstacle otherwise)
         uint32_t cut_aa = __float_as_uint(q.cut2_aa), cut_ao = __float_as_uint(q.cut2_ao);
         asm volatile("" : "+v"(cut_aa), "+v"(cut_ao));
-        (void)cutb;
         uint32_t rw = 0, cw = 0, nz = 0;
 #pragma unroll
         for (int c = M - 1; c >= 0; --c) {   // descending: column c ends at bit c
@@ -1802,14 +1800,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
 
     GSM_RSTAMP(p, wid, 8);
     for (int k = 0; k < K; ++k) {
-        // the hand-off loads of this iteration, in flight during the step
-        XferOff xo{0ull, 0ull, 0ull};
-        uint64_t gl = 0;
-        if (k >= 2) xo = xfer_off_load(xf(), k - 2, w, lane);
-        if (k >= 1 && glast) gl = xfer_grp_load(xf(), k - 1, w, lane);
         GSM_TNOW(tc0);
         const int nrow = arow + 1 == n_act ? 0 : arow + 1;
         const float4 anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, agent ? m : 0);
+        // the hand-off loads of this iteration, in flight during the step
+        // (issued after the action load, whose wait then leaves them pending:
+        // the vector memory counter drains in order)
+        // (unconditional, at valid addresses: a load under a branch leaves the
+        // compiler's count of outstanding loads unknown at the join, and every
+        // later wait becomes a full drain)
+        const XferOff xo = xfer_off_load_all(xf(), k >= 2 ? k - 2 : 0, w, lane);
+        const uint64_t gl = xfer_grp_load(xf(), k >= 1 ? k - 1 : 0, w, lane);
         const float2 *const s_cur = pos_buf(cur);
         float2 *const s_pos = pos_buf(next_buf(cur));
         KernargParams &pc = late_params();
