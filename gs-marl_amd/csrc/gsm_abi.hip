@@ -410,8 +410,8 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
         if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, gsm::block_threads(p), lds);
         if (e != hipSuccess) return hip_fail(h, e, "occupancy query (eager rollout)");
         if ((int64_t)per_cu * n_cu < nb) return kEagerIneligible;
-        // (tile look-back: aggregates + inclusive prefixes per workgroup;
-        // segmented: per-wave counts + group sums)
+        // (look-back: aggregates + inclusive prefixes per workgroup; packed
+        // small envs: per-wave counts + group sums)
         const size_t xw = (size_t)nb * gsm::kWavesPerBlock;
         const size_t bytes = 16 + std::max(2 * (size_t)nb, xw + (xw + gsm::kWave - 1) / gsm::kWave) * sizeof(uint64_t);
         e = hipMalloc(&h->eager_gran, bytes);
@@ -787,11 +787,13 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         if (fallback) return kRollIneligible;
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: n_steps must be <= 4094");
     }
-    // segmented and ragged: per-wave granules, groups of 64 waves (at most 128
-    // groups: one residency round holds <= 8192 waves); ragged: edges packed
-    // `depth` steps late
+    // ragged and packed small envs: per-wave granules, groups of 64 waves (at
+    // most 128 groups: one residency round holds <= 8192 waves); ragged: edges
+    // packed `depth` steps late
     const int xW = nb * gsm::kWavesPerBlock, xNG = (xW + gsm::kWave - 1) / gsm::kWave;
-    const bool per_wave = !tile;   // per-wave granules (Xfer); the tile rollout looks back per workgroup
+    // per-wave granules (Xfer): ragged and packed small envs; the other
+    // segmented shapes and the tile path look back per workgroup
+    const bool per_wave = ragged || (!tile && gsm::roll_packed(p));
     if (per_wave && xNG > 2 * gsm::kWave) {
         if (fallback) return kRollIneligible;
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: more than 8192 envs in one rollout launch");
@@ -847,8 +849,8 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     }
     gsm_handle::Slot &sl = h->slots[slot];
     drop_slot(sl);
-    // a 16-byte header (unused), then 8-byte granules. Segmented and ragged:
-    // per-wave counts [K][xW] and group sums [K][xNG]; tile:
+    // a 16-byte header (unused), then 8-byte granules. Ragged and packed
+    // small envs: per-wave counts [K][xW] and group sums [K][xNG]; others:
     // aggregates [K][nb] and inclusive prefixes [K][nb] (look-back). Zeroed
     // once here — granules are tagged with the launch epoch, so replays never
     // clear them

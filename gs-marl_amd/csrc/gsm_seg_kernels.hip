@@ -1162,9 +1162,9 @@ __device__ __forceinline__ float2 roll_force(const Params &p, float4 a, bool age
 }
 
 // LDS per wave of the segmented rollout: [positions E | staging scratch 28 E]
-// rounded to 16 B, then [positions E | next forces N | positions E]
+// rounded to 16 B, then [positions E | next forces N]
 constexpr int roll_lds_step(int E) { return (36 * E + 15) & ~15; }
-constexpr int roll_lds_wave(int N, int E) { return roll_lds_step(E) + 16 * E + 8 * N; }
+constexpr int roll_lds_wave(int N, int E) { return roll_lds_step(E) + 8 * E + 8 * N; }
 
 // kSlots: per-step outputs at base + k * stride (a rollout buffer); else every
 // step into the bound buffers (the strides are 0 and fold away)
@@ -1187,24 +1187,22 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     L0.live = L0.lane < M && L0.b < p.B;
     L0.agent = L0.live && L0.m < N;
     const int wave = L0.wave;
-    // Positions rotate through three LDS buffers: `cur` holds the positions
-    // before step k, step k writes its agents' new positions into the next,
-    // and the one before `cur` still holds the positions after step k - 2,
-    // whose edges iteration k writes; goals and obstacles (static within an
-    // episode) are kept in all three (a relayout reaches the other two as
-    // their pending emissions finish). Compile-time layout (roll_kernel_lds):
-    // [positions | staging scratch], [positions | the next step's agent
-    // forces | positions].
+    // Positions ping-pong between two LDS buffers: step k reads buffer k & 1
+    // and writes the agents' new positions into the other, so the previous
+    // step's positions (for its emission) need no copy; goals and obstacles
+    // (static within an episode) are kept in both. Compile-time layout
+    // (roll_kernel_lds): [positions | staging scratch], [positions | the next
+    // step's agent forces].
     constexpr int kStep = roll_lds_step(E), wstride = roll_lds_wave(N, E);
     unsigned char *wave_lds = smem + wave * wstride;
     float2 *const s_buf0 = (float2 *)wave_lds;
     float *s_nf = (float *)(s_buf0 + E);
     float2 *const s_buf1 = (float2 *)(wave_lds + kStep);
     float2 *s_force = s_buf1 + E;
-    float2 *const s_buf2 = s_force + N;
-    auto pos_buf = [&](int i) { return i == 0 ? s_buf0 : i == 1 ? s_buf1 : s_buf2; };
-    auto next_buf = [](int i) { return i == 2 ? 0 : i + 1; };
-    auto prev_buf = [](int i) { return i == 0 ? 2 : i - 1; };
+    auto pos_buf = [&](int k) { return (float2 *)(wave_lds + (k & 1) * kStep); };   // positions before step k
+    int *s_bc = (int *)(smem + kWavesPerBlock * wstride);   // [2][waves]: per-env edge counts by parity
+    int *s_red = s_bc + 2 * kWavesPerBlock;                 // [2]: the workgroup's offset (+ pad)
+    int *s_pre = s_red + 2;                                 // [2][waves]: exclusive prefix of the counts
     constexpr int scr_cap = (kStep - 8 * E) / 4;
     const bool wave_live = L0.b < p.B;
     const int64_t eb = wave_live ? L0.b : 0;
@@ -1218,8 +1216,8 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     float2 acc = in.acc, v = in.v, u = in.u;
     uint64_t cand_prev = in.cand_prev, oo = in.oo;
     if (wave_live) {
-        if (L0.lane < E) s_buf0[L0.lane] = s_buf1[L0.lane] = s_buf2[L0.lane] = in.x0;
-        if (L0.lane + kWave < E) s_buf0[L0.lane + kWave] = s_buf1[L0.lane + kWave] = s_buf2[L0.lane + kWave] = in.x1;
+        if (L0.lane < E) s_buf0[L0.lane] = s_buf1[L0.lane] = in.x0;
+        if (L0.lane + kWave < E) s_buf0[L0.lane + kWave] = s_buf1[L0.lane + kWave] = in.x1;
     }
     wave_sync();
     GSM_RSTAMP(p, L0.b, 1);
@@ -1252,39 +1250,52 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     }
 
     const int K = p.roll.K, n_act = p.roll.n_actions;
+    const uint32_t etag = roll_epoch_tag(p.roll.epoch);     // this launch's tag base
     int arow = p.roll.t_first % n_act;                      // action row of the current step
     uint8_t deg = 0;                                        // App. A S16 flags of the final state
-    // CSR hand-off per wave (gsm_device.h Xfer; env = wave): each wave
-    // publishes its env's edge count of step k in iteration k, the last wave
-    // of each group of 64 their group sum in iteration k + 1, and step k's
-    // edges are written in iteration k + 2 at the offset those give. No
-    // workgroup barrier and no look-back walk in the loop: every granule a
-    // wave reads was published an iteration before, and its loads are issued
-    // before the step's work (measured: the look-back alone cost 0.8 us of the
-    // 8.4 us step at H, profiles/r4_ab).
-    const int w = L0.b;                                     // this wave's index in the grid
-    const bool glast = (w & 63) == 63;                      // publishes its group's sums
-    auto xf = [&]() -> Xfer {
-        KernargParams &q = late_params();
-        Xfer x;
-        x.W = q.roll.xW;
-        x.NG = q.roll.xNG;
-        x.agg = q.roll.gran;
-        x.grp = x.agg + (int64_t)q.roll.K * x.W;
-        x.status = q.roll.status;
-        x.etag = roll_epoch_tag(q.roll.epoch);
-        return x;
-    };
-    uint64_t row_m2 = 0;            // radius rows of step k - 2 (oo: step k - 1)
-    int cnt_m1 = 0, cnt_m2 = 0;     // the env's edge counts of steps k - 1, k - 2
-    bool relaid_m1 = false;         // a relayout in the previous iteration
-    int cur = 0;                    // the buffer holding the positions before step k
-    // The edges of step j (positions in buffer pb, rows `rows`, `cnt` edges)
-    // at the wave's offset woff
-    auto emit = [&](const int j, const int pb, const uint64_t rows, const int cnt, const int woff, const Lane &L) {
+    // The edges of step t_first + k - 1, emitted in iteration k (k = 1..K-1)
+    // and by the tail after the loop (k = K): kept positions and row masks;
+    // the counts of this workgroup's envs are read before the exchange barrier.
+    auto emit_prev = [&](const int k, const Lane &L) {
+        const int par = k & 1;
+        const int *cb = s_bc + (1 - par) * kWavesPerBlock;   // this workgroup's counts of step t - 1
+        // the env's list staged first (needs only its own row counts)
         GSM_TNOW(te0);
-        const int staged = wave_live ? stage_rows<kN, kNo>(L, (uint32_t *)s_nf, scr_cap, rows) : -1;
-        int64_t env_off = woff;
+        const int staged = wave_live ? stage_rows<kN, kNo>(L, (uint32_t *)s_nf, scr_cap, oo) : -1;
+        GSM_ACC(p, L.b, 14, te0);   // diagnostic builds: staging (emission, below, adds to it)
+        GSM_TNOW(te1);
+        // wave 0 walks back over the predecessors, hands the workgroup's
+        // offset to the other waves and publishes its inclusive prefix
+        if (wave == 0) {
+            KernargParams &qe = late_params();
+            const int64_t kb = (int64_t)(k - 1) * gridDim.x;
+#if GSM_ABL_HANDOFF   // ablation builds only (wrong offsets): the step without the look-back
+            const int ex = 0;
+#else
+            const int ex = roll_lookback(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
+                                         etag | (uint32_t)k, qe.roll.status, L.lane);
+#endif
+            if (L.lane == 0) {
+                s_red[0] = ex;
+                __hip_atomic_store((gu64 *)(qe.roll.gran + (int64_t)K * gridDim.x + kb + blockIdx.x),
+                                   ((uint64_t)(etag | (uint32_t)k) << 32) |
+                                       (uint32_t)(ex + cb[0] + cb[1] + cb[2] + cb[3]),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
+        GSM_ACC(p, L.b, 12, te1);   // look-back (wave 0)
+        GSM_TNOW(te2);
+#if GSM_ABL_HANDOFF < 2
+        __syncthreads();
+#endif
+        GSM_ACC(p, L.b, 13, te2);   // waiting for it
+        GSM_TNOW(te3);
+        if (k == K) GSM_RSTAMP(p, L.b, 6);
+        // (the prefix formed once by thread 0, not w < wave selects: those
+        // are loop-invariant lane masks the compiler holds in SGPR pairs)
+        const int before = s_pre[(1 - par) * kWavesPerBlock + wave];
+        const int my_cnt = cb[wave];
+        int64_t env_off = (int64_t)s_red[0] + before;
         // (an offset past the capacity is a legal overflow of a small slot:
         // edge_ptr keeps it, the writes below stop at the capacity)
         if (env_off < 0) {   // a broken hand-off: never write out of bounds
@@ -1295,19 +1306,19 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         if (wave_live) {
             KernargParams &qs = late_params();
             if (L.lane == 0) {
-                int64_t *const eptr = qs.ro.eptr + (kSlots ? j * qs.ro.ep_s : 0);
+                int64_t *const eptr = qs.ro.eptr + (kSlots ? (k - 1) * qs.ro.ep_s : 0);
                 eptr[L.b] = env_off;
-                if (L.b == qs.B - 1) eptr[qs.B] = env_off + cnt;
+                if (L.b == qs.B - 1) eptr[qs.B] = env_off + my_cnt;
             }
-            const EdgeSink out = roll_edge_sink<kSlots>(qs, j, K);
-            const float2 *s_prev = pos_buf(pb);                 // positions after step j
+            const EdgeSink out = roll_edge_sink<kSlots>(qs, k - 1, K);
+            const float2 *s_prev = pos_buf(k);                  // positions after step t - 1
             if (staged >= 0 && env_off + staged <= out.cap)
                 write_staged<kN, kNo>(L, s_prev, (uint32_t *)s_nf, staged, env_off, out);
             else
-                emit_rows<kN, kNo, 1>(s, L, s_prev, rows, env_off, out, env_off + cnt > out.cap);
+                emit_rows<kN, kNo, 1>(s, L, s_prev, oo, env_off, out, env_off + my_cnt > out.cap);
         }
         wave_sync();
-        GSM_ACC(p, L.b, 14, te0);   // diagnostic builds: staging + emission
+        GSM_ACC(p, L.b, 14, te3);
     };
     for (int k = 0; k < K; ++k) {
         // lane-derived values re-formed every iteration (an asm barrier): held
@@ -1323,8 +1334,8 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
 
         // apply_environment_force + integrate_state (as gsm_step_seg_kernel):
         // from s_cur into s_pos
-        const float2 *const s_cur = pos_buf(cur);
-        float2 *const s_pos = pos_buf(next_buf(cur));
+        const float2 *const s_cur = pos_buf(k);
+        float2 *const s_pos = pos_buf(k + 1);
         KernargParams &pc = late_params();
         if (L.agent) {
             const float2 pi = s_cur[m];
@@ -1434,7 +1445,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         }
 
         // the step's observation outputs (node features, reward / cost above,
-        // done; edges two iterations on); the simulator state (positions,
+        // done; edges one iteration on); the simulator state (positions,
         // velocities, masks, counters) stays on chip and is stored once, after
         // the loop
         KernargParams &q = late_params();
@@ -1460,87 +1471,73 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             (q.ro.done + (kSlots ? k * q.ro.done_s : 0))[L.b] = done ? 1 : 0;
             if (kSlots || k == K - 1) (q.ro.ecount + (kSlots ? k * q.ro.ec_s : 0))[L.b] = wave_edges;
         }
-        GSM_ACC(p, L.b, 10, tw0);   // diagnostic builds: the step's work
+
+        // publish the workgroup's edge sum of step t
+        const int par = k & 1;
+        if (L.lane == 0) s_bc[par * kWavesPerBlock + wave] = wave_edges;
+        GSM_ACC(p, L.b, 10, tw0);   // the step's work
         GSM_TNOW(tw1);
-        // publish the env's count of this step, then (a group's last wave) the
-        // group sum of the previous step
-        // (the hand-off loads are issued here, not early in the step: held in
-        // flight through it they spill at the 64-VGPR budget of 8 waves per
-        // SIMD, and the other seven waves of the SIMD cover their latency)
-        if (L.lane == 0) xfer_st(xf().agg + (int64_t)k * xf().W + w, xf().tag(k), (uint32_t)wave_edges);
-        if (k >= 1 && glast) xfer_grp_publish(xf(), xfer_grp_load(xf(), k - 1, w, L.lane), k - 1, w, L.lane, cnt_m1);
-        GSM_ACC(p, L.b, 11, tw1);   // publish
+#if GSM_ABL_HANDOFF < 2
+        __syncthreads();
+#endif
+        GSM_ACC(p, L.b, 11, tw1);   // the publish barrier
+        if (threadIdx.x == 0) {
+            int sum = 0;
+            for (int w = 0; w < kWavesPerBlock; ++w) {
+                s_pre[par * kWavesPerBlock + w] = sum;
+                sum += s_bc[par * kWavesPerBlock + w];
+            }
+            __hip_atomic_store((gu64 *)(q.roll.gran + (int64_t)k * gridDim.x + blockIdx.x),
+                               ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)sum, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+            // the last step's sums for the emit launch that follows, in the
+            // config's workgroup layout: with G envs per wave the last of the
+            // G rollout workgroups of a slot adds the others' granules
+            if (k == K - 1) {
+                const int G = q.G, r = (int)blockIdx.x;
+                if (G == 1) {
+                    q.block_edge_sum[r] = sum;
+                } else {
+                    const int first = (r / G) * G, last = min(first + G, (int)gridDim.x) - 1;
+                    if (r == last) {
+                        const uint64_t *gk = q.roll.gran + (int64_t)k * gridDim.x;
+                        const uint32_t tag = etag | (uint32_t)(k + 1);
+                        int tot = sum;
+                        for (int j = first; j < r; ++j) {
+                            uint64_t x = __hip_atomic_load((const gu64 *)(gk + j), __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT);
+                            if ((uint32_t)(x >> 32) != tag) x = roll_wait(gk + j, tag, q.roll.status);
+                            tot += (int)(uint32_t)x;
+                        }
+                        q.block_edge_sum[r / G] = tot;
+                    }
+                }
+            }
+        }
         if (k == K - 1) GSM_RSTAMP(p, L.b, 4);
-        // the edges of step k - 2 (positions in the buffer before `cur`)
-        if (k >= 2) {
-            GSM_TNOW(tw2);
-            const int woff = xfer_off_settle(xf(), xfer_off_load(xf(), k - 2, w, L.lane), k - 2, w, L.lane);
-            GSM_ACC(p, L.b, 13, tw2);   // the offset settled
-            emit(k - 2, prev_buf(cur), row_m2, cnt_m2, woff, L);
-        }
-        // a relayout in this iteration or the last: its goals and obstacles
-        // into the buffer just emitted from (the next step's s_pos)
-        if (__builtin_expect(relaid || relaid_m1, 0)) {   // wave-uniform
-            float2 *const s_nx = pos_buf(prev_buf(cur));
-            for (int e = N + m; e < E; e += kWave) s_nx[e] = s_pos[e];
-        }
-        relaid_m1 = relaid;
-        // keep step k for the next iteration's sweep and the emissions
-        row_m2 = oo;
+        if (k > 0) emit_prev(k, L);
+        // keep step t for the next iteration's emission and sweep
         oo = row;
-        cnt_m2 = cnt_m1;
-        cnt_m1 = wave_edges;
         cand_prev = L.agent ? cand : 0ull;
+        if (__builtin_expect(relaid, 0)) {   // wave-uniform: the new episode's statics into the other buffer
+            for (int e = N + m; e < E; e += kWave) pos_buf(k)[e] = s_pos[e];
+        }
         if constexpr (!kFused) u = roll_force<kFmt>(late_params(), anext, L.agent);
         arow = nrow;
-        cur = next_buf(cur);
         wave_sync();
     }
-    // the tail: the group sums of the last step, then the edges of the last
-    // two steps
-    const int fin = cur;   // positions after the last step
-    {
+    {   // the tail: the last step's edges
         Lane L = L0;
         asm volatile("" : "+v"(L.lane), "+v"(L.m));
         GSM_RSTAMP(p, L.b, 5);
-        for (int k = K; k < K + 2; ++k) {
-            const XferOff xo = xfer_off_load_all(xf(), k >= 2 ? k - 2 : 0, w, L.lane);
-            if (k == K && K >= 1 && glast)
-                xfer_grp_publish(xf(), xfer_grp_load(xf(), K - 1, w, L.lane), K - 1, w, L.lane, cnt_m1);
-            if (k >= 2) {
-                const int woff = xfer_off_settle(xf(), xo, k - 2, w, L.lane);
-                if (k == K + 1) GSM_RSTAMP(p, L.b, 6);
-                emit(k - 2, prev_buf(cur), row_m2, cnt_m2, woff, L);
-            }
-            row_m2 = oo;
-            cnt_m2 = cnt_m1;
-            cur = next_buf(cur);
-        }
+        emit_prev(K, L);
         GSM_RSTAMP(p, L.b, 7);
-        // the last step's sums for an emit launch that follows, in the
-        // config's workgroup layout (4 waves of G envs: rollout waves
-        // [4G j, 4G (j + 1)) are its workgroup j), by the last wave of each
-        if (K >= 1) {
-            KernargParams &q = late_params();
-            const int span = kWavesPerBlock * q.G, W = q.roll.xW;
-            if (w % span == span - 1 || w == W - 1) {
-                const int first = w - w % span;
-                const Xfer x = xf();
-                const uint64_t *ag = x.agg + (int64_t)(K - 1) * x.W + first;
-                const int n = w - first;   // < 64
-                const uint64_t l = xfer_ld(ag + min(L.lane, n > 0 ? n - 1 : 0));
-                const int tot = wave_total((int)xfer_settle(l, ag + min(L.lane, n > 0 ? n - 1 : 0), L.lane < n,
-                                                            x.tag(K - 1), x.status)) +
-                                cnt_m1;
-                if (L.lane == 0) q.block_edge_sum[w / span] = tot;
-            }
-        }
     }
     // the final state (what the next launch or an eager step reads)
     KernargParams &q = late_params();
     if (wave_live) {
         float2 *const pos_b = q.pos + eb * E;
-        const float2 *const s_pos = pos_buf(fin);
+        const float2 *const s_pos = pos_buf(K);
         if (L0.lane < E) pos_b[L0.lane] = s_pos[L0.lane];
         if (L0.lane + kWave < E) pos_b[L0.lane + kWave] = s_pos[L0.lane + kWave];
         if (L0.agent) {
@@ -1574,8 +1571,9 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
 // same envs (G = 4 there too: a workgroup holds the same 16 envs, so the last
 // step's workgroup sums are the config's block_edge_sum directly).
 constexpr int kPackSeg = 16, kPackG = kWave / kPackSeg;   // lanes per env, envs per wave
+constexpr int kPackDepth = 4;   // iterations between a step and the writing of its edges
 template <int kN, int kNo>
-constexpr int pack_lds_wave() { return 4 * 8 * kPackG * (2 * kN + kNo) + 8 * kPackG * kN; }
+constexpr int pack_lds_wave() { return (kPackDepth + 1) * 8 * kPackG * (2 * kN + kNo) + 8 * kPackG * kN; }
 template <int kCtrl>
 __device__ __forceinline__ int dpp_row0(int v) {   // DPP within 16-lane rows, 0 shifted in
     return __builtin_amdgcn_update_dpp(0, v, kCtrl, 0xf, 0xf, true);
@@ -1615,15 +1613,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const bool env_live = b < p.B;
     const bool live = env_live && m < M, agent = live && m < N;
     const int64_t eb = env_live ? b : 0;
-    // LDS per wave: positions [4][G][E] in rotation — buffer `cur` holds the
-    // positions before step k, step k writes all of its env's rows into the
-    // next (agents integrated, goals / obstacles carried or relaid), and the
-    // two before `cur` still hold the positions after steps k - 2 and k - 3
-    // (this iteration emits step k - 3's edges) — then the next step's forces
-    // [G][N]
+    // LDS per wave: positions [kPackDepth + 1][G][E] in rotation — buffer
+    // `cur` holds the positions before step k, step k writes all of its env's
+    // rows into the next (agents integrated, goals / obstacles carried or
+    // relaid), and the others still hold the positions after steps k - 2 ..
+    // k - kPackDepth (this iteration writes step k - kPackDepth's edges) —
+    // then the next step's forces [G][N]
     float2 *const s_w = (float2 *)(smem + wave * pack_lds_wave<kN, kNo>());
     auto pos_buf = [&](int i) { return s_w + i * kPackG * E + seg * E; };   // this env's rows in buffer i
-    float2 *const s_force = s_w + 4 * kPackG * E + seg * N;
+    float2 *const s_force = s_w + (kPackDepth + 1) * kPackG * E + seg * N;
     int *s_bc = (int *)(smem + kWavesPerBlock * pack_lds_wave<kN, kNo>());   // [waves]: the last step's counts
     const int ent = m < N ? m : N + m;                                       // this lane's collider entity
     const int wid = blockIdx.x * kWavesPerBlock + wave;                     // (diagnostic stamps)
@@ -1718,12 +1716,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     // CSR hand-off per wave (gsm_device.h Xfer: each wave publishes its four
     // envs' edge count of step k in iteration k, the last wave of each group
     // of 64 their group sum in iteration k + 2, and step k's edges are written
-    // in iteration k + 3 at the offset those give) — no workgroup barrier and
-    // no look-back walk in the loop: every granule a wave reads was published
-    // at least an iteration before, and its loads are issued before the step's
-    // work. (Group sums one iteration on and edges two — the segmented
-    // rollout's lags — left a C2 step short of the publish-to-load latency:
-    // nearly every step re-polled its offset, ~2200 cycles.)
+    // in iteration k + 4 at the offset those give) — no workgroup barrier and
+    // no look-back walk in the loop. A hand-off hop under load takes 2-3 us
+    // (MI355X_MICROARCH.md handoff-1to1), a C2 step about 3: every granule a
+    // wave reads was published at least an iteration before it is loaded, and
+    // the loads are issued at the end of the iteration before the one that
+    // uses them, behind the next step's action load (the vector memory
+    // counter drains in order, so that load's wait leaves them in flight).
+    // (Edges two or three iterations late, loads at the iteration's start:
+    // nearly every step waited ~2000 cycles for its offset, profiles/r4_stamps.)
     const int w = blockIdx.x * kWavesPerBlock + wave;      // this wave's index in the grid
     const bool glast = (w & 63) == 63;                      // publishes its group's sums
     auto xf = [&]() -> Xfer {
@@ -1737,11 +1738,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         x.etag = roll_epoch_tag(q.roll.epoch);
         return x;
     };
-    uint32_t row_m1 = 0, row_m2 = 0, row_m3 = 0;   // radius row bits of steps k - 1, k - 2, k - 3
-    int cnt_m1 = 0, cnt_m2 = 0;                    // this wave's edge counts of steps k - 1, k - 2
+    uint32_t row_m1 = 0, row_m2 = 0, row_m3 = 0, row_m4 = 0;   // radius row bits of steps k - 1 .. k - 4
+    int cnt_m1 = 0, cnt_m2 = 0;                                // this wave's edge counts of steps k - 1, k - 2
     uint32_t cand_keep = cand_prev;
     bool coinc = false;
-    int cur = 0;   // the buffer holding the positions before step k (those after step k - 3: cur + 2)
+    static_assert(kPackDepth == 4, "the row ring below");
+    auto ring = [](int i) { return i >= kPackDepth + 1 ? i - (kPackDepth + 1) : i; };
+    int cur = 0;   // the buffer holding the positions before step k (those after step k - 4: cur + 2)
 
     // the edges of step j (positions in buffer `pb`, rows `row`) at the wave's
     // offset `woff`: each env after the wave's earlier envs
@@ -1804,20 +1807,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     };
 
     GSM_RSTAMP(p, wid, 8);
+    // the first iteration's next-step actions and hand-off loads (the loads
+    // unconditional, at valid addresses: a load under a branch leaves the
+    // compiler's count of outstanding loads unknown at the join, and every
+    // later wait becomes a full drain)
+    int nrow = arow + 1 == n_act ? 0 : arow + 1;
+    float4 anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, agent ? m : 0);
+    XferOff xo = xfer_off_load_all(xf(), 0, w, lane);
+    uint64_t gl = xfer_grp_load(xf(), 0, w, lane);
     for (int k = 0; k < K; ++k) {
         GSM_TNOW(tc0);
-        const int nrow = arow + 1 == n_act ? 0 : arow + 1;
-        const float4 anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, agent ? m : 0);
-        // the hand-off loads of this iteration, in flight during the step
-        // (issued after the action load, whose wait then leaves them pending:
-        // the vector memory counter drains in order)
-        // (unconditional, at valid addresses: a load under a branch leaves the
-        // compiler's count of outstanding loads unknown at the join, and every
-        // later wait becomes a full drain)
-        const XferOff xo = xfer_off_load_all(xf(), k >= 3 ? k - 3 : 0, w, lane);
-        const uint64_t gl = xfer_grp_load(xf(), k >= 2 ? k - 2 : 0, w, lane);
         const float2 *const s_cur = pos_buf(cur);
-        float2 *const s_pos = pos_buf((cur + 1) & 3);
+        float2 *const s_pos = pos_buf(ring(cur + 1));
         KernargParams &pc = late_params();
         // apply_environment_force (formed by the previous sweep) + integrate_state;
         // goals and obstacles carried into the step's buffer
@@ -1926,38 +1927,47 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (lane == 0) xfer_st(xf().agg + (int64_t)k * xf().W + w, xf().tag(k), (uint32_t)wcnt);
         if (k >= 2 && glast) xfer_grp_publish(xf(), gl, k - 2, w, lane, cnt_m2);
         GSM_ACC(late_params(), wid, 1, tc1);   // publish
-        // the edges of step k - 3
-        if (k >= 3) {
+        // the edges of step k - 4
+        if (k >= kPackDepth) {
             GSM_TNOW(te0);
-            const int woff = xfer_off_settle(xf(), xo, k - 3, w, lane);
+            const int woff = xfer_off_settle(xf(), xo, k - kPackDepth, w, lane);
             GSM_ACC(late_params(), wid, 3, te0);   // the offset settled
-            emit(k - 3, (cur + 2) & 3, row_m3, woff);
+            emit(k - kPackDepth, ring(cur + 2), row_m4, woff);
         }
+        row_m4 = row_m3;
         row_m3 = row_m2;
         row_m2 = row_m1;
         row_m1 = rad;
         cnt_m2 = cnt_m1;
         cnt_m1 = wcnt;
         cand_keep = cand;
-        cur = (cur + 1) & 3;
+        cur = ring(cur + 1);
         arow = nrow;
+        // the next iteration's next-step actions, then its hand-off loads
+        nrow = arow + 1 == n_act ? 0 : arow + 1;
+        anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, agent ? m : 0);
+        xo = xfer_off_load_all(xf(), k + 1 >= kPackDepth ? k + 1 - kPackDepth : 0, w, lane);
+        gl = xfer_grp_load(xf(), k + 1 >= 2 ? k - 1 : 0, w, lane);
         wave_sync();
     }
     // the tail: the group sums of the last two steps, then the edges of the
-    // last three
+    // last four (the first tail iteration's loads were issued by the loop)
     const int fin = cur;   // positions after the last step
     const int last_cnt = cnt_m1;
     const uint32_t last_row = row_m1;
-    for (int k = K; k < K + 3; ++k) {
-        XferOff xo{0ull, 0ull, 0ull};
-        if (k >= 3) xo = xfer_off_load(xf(), k - 3, w, lane);
-        if (k - 2 >= 0 && k - 2 < K && glast)
-            xfer_grp_publish(xf(), xfer_grp_load(xf(), k - 2, w, lane), k - 2, w, lane, cnt_m2);
-        if (k >= 3) emit(k - 3, (cur + 2) & 3, row_m3, xfer_off_settle(xf(), xo, k - 3, w, lane));
+    for (int k = K; k < K + kPackDepth; ++k) {
+        if (k > K) {
+            xo = xfer_off_load_all(xf(), k >= kPackDepth ? k - kPackDepth : 0, w, lane);
+            gl = xfer_grp_load(xf(), k >= 2 ? k - 2 : 0, w, lane);
+        }
+        if (k - 2 >= 0 && k - 2 < K && glast) xfer_grp_publish(xf(), gl, k - 2, w, lane, cnt_m2);
+        if (k >= kPackDepth)
+            emit(k - kPackDepth, ring(cur + 2), row_m4, xfer_off_settle(xf(), xo, k - kPackDepth, w, lane));
+        row_m4 = row_m3;
         row_m3 = row_m2;
         row_m2 = row_m1;
         cnt_m2 = cnt_m1;
-        cur = (cur + 1) & 3;
+        cur = ring(cur + 1);
     }
     GSM_RSTAMP(p, wid, 9);
     // the last step's sums in the config's workgroup layout (G = 4: the same
@@ -2054,7 +2064,7 @@ size_t roll_kernel_lds(const DevParams &p) {
     if (p.N == n && p.No == no) return (size_t)kWavesPerBlock * pack_lds_wave<n, no>() + 4 * kWavesPerBlock;
     GSM_PACK_SHAPES(GSM_PICK)
 #undef GSM_PICK
-    return (size_t)kWavesPerBlock * roll_lds_wave(p.N, p.E);
+    return (size_t)kWavesPerBlock * roll_lds_wave(p.N, p.E) + 4 * (4 * kWavesPerBlock + 2);
 }
 
 const void *emit_seg_kernel_fn(const DevParams &p) {

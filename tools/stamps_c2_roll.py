@@ -2,9 +2,9 @@
 batch (navigation, 3 agents x 4096 envs, four envs per wave; diagnostic
 -DGSM_STAMPS build, run with GSM_LIB_PATH pointing at it). One 100-step launch
 after a warm one; per wave, s_memtime cycles summed per phase over the steps
-(gsm_seg_kernels.hip gsm_roll_pack_kernel): the step's work, the publish
-barrier, the look-back (wave 0 of each workgroup), the wait for it, the
-emission; and the lifetime (s_memrealtime, 100 MHz).
+(gsm_seg_kernels.hip gsm_roll_pack_kernel): the step's work, the hand-off
+publishes, the settle of the offset granules, the emission; and the lifetime
+(s_memrealtime, 100 MHz).
 
 Usage: GSM_LIB_PATH=.../ablate/stamps.so python tools/stamps_c2_roll.py"""
 import ctypes as C
@@ -38,7 +38,7 @@ s1.record()
 torch.cuda.synchronize()
 assert not env.roll_gave_up()
 q = st.cpu().numpy().astype(np.int64)
-names = ["work", "publish_barrier", "lookback", "lookback_wait", "emit"]
+names = ["work", "publish", "unused", "offset_settle", "emit"]
 t0 = q[:, 8].min()
 start, end = (q[:, 8] - t0) / 100.0, (q[:, 9] - t0) / 100.0
 w0 = np.arange(W) % 4 == 0
