@@ -376,6 +376,17 @@ int redirect(gsm_handle *h, gsm::DevParams *p, const gsm_outputs *o) {
 uint32_t next_launch_epoch();
 hipError_t clear_status(gsm_handle *h);
 
+// The rollout granules (in-launch hand-off words, gsm_device.h): GSM_GRAN_MEM
+// = "uncached" or "fine" allocates them uncached / fine-grained instead of
+// hipMalloc's default (an A/B knob: a cached line of another XCD's granules
+// can serve an agent-scope load stale until it leaves this XCD's L2)
+hipError_t gran_malloc(void **p, size_t bytes) {
+    const char *ev = getenv("GSM_GRAN_MEM");
+    if (ev && !strcmp(ev, "uncached")) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+    if (ev && !strcmp(ev, "fine")) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocFinegrained);
+    return hipMalloc(p, bytes);
+}
+
 // gsm_step as ONE launch (opt-in, GSM_EAGER_ONE_LAUNCH=1): the config's fused
 // rollout kernel with K = 1 (the step, then its edges at the CSR offset of the
 // in-launch look-back) instead of the step kernel + the emit kernel — the same
@@ -414,7 +425,7 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
         // small envs: per-wave counts + group sums)
         const size_t xw = (size_t)nb * gsm::kWavesPerBlock;
         const size_t bytes = 16 + std::max(2 * (size_t)nb, xw + (xw + gsm::kWave - 1) / gsm::kWave) * sizeof(uint64_t);
-        e = hipMalloc(&h->eager_gran, bytes);
+        e = gran_malloc((void **)&h->eager_gran, bytes);
         if (e != hipSuccess) { h->eager_gran = nullptr; return hip_fail(h, e, "hipMalloc (eager granules)"); }
         e = gsm::launch_granule_init(h->eager_gran, bytes, 0u, nullptr);
         if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
@@ -857,7 +868,7 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     // (ragged: then the placement words, gsm::PlaceArea)
     const size_t gran_alloc = 16 + (size_t)K * (per_wave ? (size_t)(xW + xNG) : 2 * (size_t)nb) * sizeof(uint64_t) +
                               (ragged ? gsm::PlaceArea::words(xW) * sizeof(uint64_t) : 0);
-    e = hipMalloc(&sl.gran, gran_alloc);
+    e = gran_malloc((void **)&sl.gran, gran_alloc);
     if (e != hipSuccess) {
         sl.gran = nullptr;
         if (fallback) return kRollIneligible;   // the per-step chain needs no granules
