@@ -376,15 +376,17 @@ int redirect(gsm_handle *h, gsm::DevParams *p, const gsm_outputs *o) {
 uint32_t next_launch_epoch();
 hipError_t clear_status(gsm_handle *h);
 
-// The rollout granules (in-launch hand-off words, gsm_device.h): GSM_GRAN_MEM
-// = "uncached" or "fine" allocates them uncached / fine-grained instead of
-// hipMalloc's default (an A/B knob: a cached line of another XCD's granules
-// can serve an agent-scope load stale until it leaves this XCD's L2)
+// The rollout granules (in-launch hand-off words, gsm_device.h) are allocated
+// uncached: an agent-scope load of a granule line that this XCD's L2 still
+// holds from an earlier read can be served stale until the line leaves the
+// L2, and the hand-off then re-polls. Same box, one run each (profiles/
+// r4_gran): C2 3.44 -> 3.16 us per step, H 8.46 -> 8.31, C3 and C4 within
+// noise. GSM_GRAN_MEM = "hip" / "fine" selects hipMalloc / fine-grained (A/B).
 hipError_t gran_malloc(void **p, size_t bytes) {
     const char *ev = getenv("GSM_GRAN_MEM");
-    if (ev && !strcmp(ev, "uncached")) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+    if (ev && !strcmp(ev, "hip")) return hipMalloc(p, bytes);
     if (ev && !strcmp(ev, "fine")) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocFinegrained);
-    return hipMalloc(p, bytes);
+    return hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
 }
 
 // gsm_step as ONE launch (opt-in, GSM_EAGER_ONE_LAUNCH=1): the config's fused

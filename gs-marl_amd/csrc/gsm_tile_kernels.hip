@@ -22,8 +22,6 @@
 //
 // Same arithmetic contract as the other paths (d2 = dx*dx + dy*dy without
 // contraction, squared predicates).
-#include <type_traits>
-
 #include "gsm_device.h"
 
 namespace gsm {
@@ -203,15 +201,10 @@ __device__ __forceinline__ uint64_t agent_bits_of_word(int N, int k) {   // agen
     const int M = N + No, E = 2 * N + No;                                 \
     const int W = kN > 0 ? (kN + kNo + 63) / 64 : (p).W;                  \
     (void)M, (void)E, (void)W, (void)No
-// Side (not int): the workgroup's last wave runs side() instead of sweeping,
-// and the column units go to the other waves (the column pass issues on the
-// CU's shared scalar path, so seven waves take no longer than eight: the side
-// work is free when it fits the pass)
-template <int kN = 0, int kNo = 0, typename Side = int>
+template <int kN = 0, int kNo = 0>
 __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s_pos, const TileSymLds &S,
                                              int *s_cost, int64_t eb, bool keep_oo, uint64_t *rout = nullptr,
-                                             const uint64_t *rkeep = nullptr, uint64_t *cout = nullptr,
-                                             Side side = 0) {
+                                             const uint64_t *rkeep = nullptr, uint64_t *cout = nullptr) {
     typedef float f32x2 __attribute__((ext_vector_type(2)));
     GSM_TILE_SHAPE(p);
     const int tid = threadIdx.x, lane = tid & 63;
@@ -230,12 +223,7 @@ __device__ __forceinline__ int obs_sweep_sym(const DevParams &p, const float2 *s
     const float R2 = p.R2;
     const int U = W * NB8;
     GSM_TNOW(ts0);
-    constexpr bool kSide = !std::is_same<Side, int>::value;
-    constexpr int kSweepWaves = kSide ? kTileWaves - 1 : kTileWaves;
-    if constexpr (kSide) {
-        if (wave == kTileWaves - 1) side();
-    }
-    for (int u = wave; u < (kSide && wave == kTileWaves - 1 ? 0 : U); u += kSweepWaves) {
+    for (int u = wave; u < U; u += kTileWaves) {
         const int c = u / NB8, jb = u - c * NB8;
         const int m = 64 * c + lane;
         const bool live = m < M, obst = live && m >= N;
@@ -863,12 +851,11 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         uint64_t *const rout = s_rm + (k & 1) * M * W;
         const uint64_t *const rkeep = s_rm + ((k + 1) & 1) * M * W;   // the previous step's masks
         int edges = 0;
-        // the previous step's CSR offset: the look-back by the last wave, in
-        // place of its share of the sweep's column pass (below; the tail: here),
-        // read by the emission after the step (s_x[2], published by the step's
-        // barriers)
-        auto lookback = [&]() {
-            if (k == 0) return;
+        // the previous step's CSR offset: the look-back by the last wave, idle
+        // in the physics below (agents 0..N-1 on the first threads), so its
+        // latency overlaps the step; read by the emission after the step
+        // (s_x[2], published by the step's barriers)
+        if (k > 0 && wave == kTileWaves - 1) {
             GSM_TNOW(tp4);
             const int64_t kb = (int64_t)(k - 1) * gridDim.x;
             KernargParams &q = late_params();
@@ -889,11 +876,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                 s_x[2] = ex;
             }
             GSM_ACC(late_params(), wid, 5, tp4);   // look-back (last wave)
-        };
-        if (k == K) {   // the tail: no step
-            if (wave == kTileWaves - 1) lookback();
-            __syncthreads();
         }
+        if (k == K) __syncthreads();   // (the tail: no step; s_x[2] for the emission)
         if (k < K) {
         bool relaid = false;
         auto relayout = [&]() {   // scenario.reset_world with the Philox layout
@@ -957,7 +941,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         const bool done = t >= late_params().EL;
         GSM_ACC(late_params(), wid, 0, tp0);   // physics
         GSM_TNOW(tp1);
-        int pairs = obs_sweep_sym<kN, kNo>(p, s_pos, sym, s_cost, eb, true, rout, rkeep, s_cm, lookback);
+        int pairs = obs_sweep_sym<kN, kNo>(p, s_pos, sym, s_cost, eb, true, rout, rkeep, s_cm);
         GSM_ACC(late_params(), wid, 2, tp1);   // sweep (column pass: 1)
         GSM_TNOW(tp2);
         auto nonfinite_part = [&]() {
