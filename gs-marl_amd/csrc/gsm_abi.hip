@@ -100,12 +100,16 @@ int align16(int x) { return (x + 15) & ~15; }
 //
 // The same upload carries the ragged rollout's placement order (after the nb
 // block entries): the grid's W = 4 * ceil(B / 4) envs by descending cost per
-// step, linear in N_env per family. Uniform polygon / line batches put
-// polygon/line at ~63 + 27 N (tools/probe_c4_balance.py); navigation envs
-// cannot be run alone on this path, and a scan of the C4 launch time over
-// the navigation weights (`tools/gpu.sh envsweep TAG c4 GSM_PLACE_MODEL ...`) put them at 55 + 18 N
-// (20 + 7 N: 39.4 us per step, 55 + 18 N: 36.9, 70 + 24 N: 38.9); padding
-// envs (b >= B) last. roll_place (gsm_ragged_kernels.hip) deals them to the
+// step, linear in N_env per family: polygon / line a + b N, navigation
+// c + d N, from scans of the C4 launch time (`tools/gpu.sh envsweep TAG c4
+// GSM_PLACE_MODEL a,b,c,d`). Round 3 (navigation sweep on the scalar path):
+// 63 + 27 N and 55 + 18 N (20 + 7 N: 39.4 us per step, 55 + 18 N: 36.9,
+// 70 + 24 N: 38.9). Round 4, with the navigation sweep and the assignment's
+// passes off the scalar path the navigation envs cost a fraction of an
+// assignment env and the assignment's cost is flatter in N
+// (profiles/r4_stamps/stamps_c4.json): 200 + 20 N and 10 + 3 N, 27.2 us per
+// step against 29.4 for the round-3 weights (profiles/r4_place); padding envs
+// (b >= B) last. roll_place (gsm_ragged_kernels.hip) deals them to the
 // SIMDs in strata.
 int update_block_order(gsm_handle *h, hipStream_t s) {
     const gsm::DevParams &p = h->dp;
@@ -116,7 +120,7 @@ int update_block_order(gsm_handle *h, hipStream_t s) {
     // cost units per env and step: polygon/line a + b N, navigation c + d N,
     // the C4 rollout's best of a scan (tools/gpu.sh envsweep,
     // GSM_PLACE_MODEL="a,b,c,d" overrides)
-    int64_t ma = 63, mb = 27, mc = 55, md = 18;
+    int64_t ma = 200, mb = 20, mc = 10, md = 3;
     if (const char *ev = getenv("GSM_PLACE_MODEL")) {
         long long x[4];
         if (sscanf(ev, "%lld,%lld,%lld,%lld", &x[0], &x[1], &x[2], &x[3]) == 4) {
