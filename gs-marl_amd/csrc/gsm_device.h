@@ -402,22 +402,8 @@ __device__ __forceinline__ void xfer_grp_publish(const Xfer &x, uint64_t l, int 
 // pays one load latency per round, was measured slower at H — four windows
 // every round: 10.2 vs 9.8 us per step; eight per round after a first single
 // window: 8.6 vs 8.4 — and for the one-launch eager step)
-// The first window's two granule loads, issued ahead of the walk (the caller
-// does other work while they are in flight, e.g. staging its edge list)
-struct LookbackPre {
-    uint64_t xi, xa;
-};
-__device__ __forceinline__ LookbackPre roll_lookback_issue(const uint64_t *agg_k, const uint64_t *inc_k, int lane) {
-    const int idx = (int)blockIdx.x - 1 - lane;
-    const int ci = idx >= 0 ? idx : 0;
-    LookbackPre pre;
-    pre.xi = __hip_atomic_load((const gu64 *)(inc_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    pre.xa = __hip_atomic_load((const gu64 *)(agg_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return pre;
-}
-template <bool kPre = false>
 __device__ __forceinline__ int roll_lookback(const uint64_t *agg_k, const uint64_t *inc_k, uint32_t tag,
-                                             uint32_t *status, int lane, LookbackPre pre = {0ull, 0ull}) {
+                                             uint32_t *status, int lane) {
     int acc = 0;
     int first = (int)blockIdx.x;
     asm volatile("" : "+s"(first));   // no window predicates hoisted into a rollout's loop (SGPR pairs)
@@ -425,14 +411,8 @@ __device__ __forceinline__ int roll_lookback(const uint64_t *agg_k, const uint64
         const int idx = hi - 1 - lane;                      // lane 0 = nearest predecessor
         const int ci = idx >= 0 ? idx : 0;
         const bool valid = idx >= 0;
-        uint64_t xi, a;
-        if (kPre && hi == first) {
-            xi = pre.xi;
-            a = pre.xa;
-        } else {
-            xi = __hip_atomic_load((const gu64 *)(inc_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            a = __hip_atomic_load((const gu64 *)(agg_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        const uint64_t xi = __hip_atomic_load((const gu64 *)(inc_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t a = __hip_atomic_load((const gu64 *)(agg_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const uint64_t have = __ballot(valid && (uint32_t)(xi >> 32) == tag);
         const int j = have ? __builtin_ctzll(have) : kWave;   // wave-uniform
         // aggregates of lanes < j (all valid lanes when no inclusive was found)

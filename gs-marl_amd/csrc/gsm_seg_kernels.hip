@@ -1259,14 +1259,6 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     auto emit_prev = [&](const int k, const Lane &L) {
         const int par = k & 1;
         const int *cb = s_bc + (1 - par) * kWavesPerBlock;   // this workgroup's counts of step t - 1
-        // wave 0's first look-back window in flight while the env's list is
-        // staged (staging touches no global memory, so no wait drains it)
-        LookbackPre pre{0ull, 0ull};
-        if (wave == 0) {
-            KernargParams &qe = late_params();
-            const int64_t kb = (int64_t)(k - 1) * gridDim.x;
-            pre = roll_lookback_issue(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb, L.lane);
-        }
         // the env's list staged first (needs only its own row counts)
         GSM_TNOW(te0);
         const int staged = wave_live ? stage_rows<kN, kNo>(L, (uint32_t *)s_nf, scr_cap, oo) : -1;
@@ -1279,10 +1271,9 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             const int64_t kb = (int64_t)(k - 1) * gridDim.x;
 #if GSM_ABL_HANDOFF   // ablation builds only (wrong offsets): the step without the look-back
             const int ex = 0;
-            (void)pre;
 #else
-            const int ex = roll_lookback<true>(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
-                                               etag | (uint32_t)k, qe.roll.status, L.lane, pre);
+            const int ex = roll_lookback(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
+                                         etag | (uint32_t)k, qe.roll.status, L.lane);
 #endif
             if (L.lane == 0) {
                 s_red[0] = ex;
