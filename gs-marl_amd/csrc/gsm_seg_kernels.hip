@@ -1207,17 +1207,6 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     const bool wave_live = L0.b < p.B;
     const int64_t eb = wave_live ? L0.b : 0;
     GSM_RSTAMP(p, L0.b, 0);   // diagnostic builds: the launch's timeline per wave
-#ifdef GSM_ROLL_PRIO   // A/B (temporary): wave priority by grid position
-    {
-        // 1: later workgroups first (they trail: each waits only on earlier
-        // ones, and the SIMDs pick the oldest wave first); -1: the reverse
-        int lvl = (int)(((uint32_t)blockIdx.x * 4u) / gridDim.x);
-        if (GSM_ROLL_PRIO < 0) lvl = 3 - lvl;
-        if (lvl == 1) __builtin_amdgcn_s_setprio(1);
-        else if (lvl == 2) __builtin_amdgcn_s_setprio(2);
-        else if (lvl == 3) __builtin_amdgcn_s_setprio(3);
-    }
-#endif
 
     // ---- the state before step t_first and step t_first's actions
     // (p.actions); the edges of that state were emitted by whatever ran before
