@@ -1571,7 +1571,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
 // same envs (G = 4 there too: a workgroup holds the same 16 envs, so the last
 // step's workgroup sums are the config's block_edge_sum directly).
 constexpr int kPackSeg = 16, kPackG = kWave / kPackSeg;   // lanes per env, envs per wave
-constexpr int kPackDepth = 4;   // iterations between a step and the writing of its edges
+constexpr int kPackDepth = 5;   // iterations between a step and the writing of its edges
 template <int kN, int kNo>
 constexpr int pack_lds_wave() { return (kPackDepth + 1) * 8 * kPackG * (2 * kN + kNo) + 8 * kPackG * kN; }
 template <int kCtrl>
@@ -1716,15 +1716,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     // CSR hand-off per wave (gsm_device.h Xfer: each wave publishes its four
     // envs' edge count of step k in iteration k, the last wave of each group
     // of 64 their group sum in iteration k + 2, and step k's edges are written
-    // in iteration k + 4 at the offset those give) — no workgroup barrier and
+    // in iteration k + 5 at the offset those give) — no workgroup barrier and
     // no look-back walk in the loop. A hand-off hop under load takes 2-3 us
-    // (MI355X_MICROARCH.md handoff-1to1), a C2 step about 3: every granule a
-    // wave reads was published at least an iteration before it is loaded, and
-    // the loads are issued at the end of the iteration before the one that
-    // uses them, behind the next step's action load (the vector memory
-    // counter drains in order, so that load's wait leaves them in flight).
-    // (Edges two or three iterations late, loads at the iteration's start:
-    // nearly every step waited ~2000 cycles for its offset, profiles/r4_stamps.)
+    // (MI355X_MICROARCH.md handoff-1to1) and a C2 step about 3: every granule
+    // a wave reads was published at least an iteration before it is loaded,
+    // and the offset loads are issued two iterations before the one that uses
+    // them (the group loads one), at the end of an iteration behind the next
+    // step's action load (the vector memory counter drains in order, so that
+    // load's wait leaves them in flight). (Edges two or three iterations
+    // late with the loads at the iteration's start, or four with them one
+    // iteration ahead: the offset still settled in ~1900-2200 cycles per
+    // step, profiles/r4_stamps.)
     const int w = blockIdx.x * kWavesPerBlock + wave;      // this wave's index in the grid
     const bool glast = (w & 63) == 63;                      // publishes its group's sums
     auto xf = [&]() -> Xfer {
@@ -1738,13 +1740,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         x.etag = roll_epoch_tag(q.roll.epoch);
         return x;
     };
-    uint32_t row_m1 = 0, row_m2 = 0, row_m3 = 0, row_m4 = 0;   // radius row bits of steps k - 1 .. k - 4
+    uint32_t row_m1 = 0, row_m2 = 0, row_m3 = 0, row_m4 = 0, row_m5 = 0;   // radius row bits of steps k - 1 .. k - 5
     int cnt_m1 = 0, cnt_m2 = 0;                                // this wave's edge counts of steps k - 1, k - 2
     uint32_t cand_keep = cand_prev;
     bool coinc = false;
-    static_assert(kPackDepth == 4, "the row ring below");
+    static_assert(kPackDepth == 5, "the row ring below");
     auto ring = [](int i) { return i >= kPackDepth + 1 ? i - (kPackDepth + 1) : i; };
-    int cur = 0;   // the buffer holding the positions before step k (those after step k - 4: cur + 2)
+    int cur = 0;   // the buffer holding the positions before step k (those after step k - 5: cur + 2)
 
     // the edges of step j (positions in buffer `pb`, rows `row`) at the wave's
     // offset `woff`: each env after the wave's earlier envs
@@ -1813,7 +1815,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     // later wait becomes a full drain)
     int nrow = arow + 1 == n_act ? 0 : arow + 1;
     float4 anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, agent ? m : 0);
+    // (the offset loads two iterations ahead: xo for this iteration, xo2 for
+    // the next — one iteration of a C2 step was shorter than such a load)
     XferOff xo = xfer_off_load_all(xf(), 0, w, lane);
+    XferOff xo2 = xfer_off_load_all(xf(), 0, w, lane);
     uint64_t gl = xfer_grp_load(xf(), 0, w, lane);
     for (int k = 0; k < K; ++k) {
         GSM_TNOW(tc0);
@@ -1927,13 +1932,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (lane == 0) xfer_st(xf().agg + (int64_t)k * xf().W + w, xf().tag(k), (uint32_t)wcnt);
         if (k >= 2 && glast) xfer_grp_publish(xf(), gl, k - 2, w, lane, cnt_m2);
         GSM_ACC(late_params(), wid, 1, tc1);   // publish
-        // the edges of step k - 4
+        // the edges of step k - 5
         if (k >= kPackDepth) {
             GSM_TNOW(te0);
             const int woff = xfer_off_settle(xf(), xo, k - kPackDepth, w, lane);
             GSM_ACC(late_params(), wid, 3, te0);   // the offset settled
-            emit(k - kPackDepth, ring(cur + 2), row_m4, woff);
+            emit(k - kPackDepth, ring(cur + 2), row_m5, woff);
         }
+        row_m5 = row_m4;
         row_m4 = row_m3;
         row_m3 = row_m2;
         row_m2 = row_m1;
@@ -1946,23 +1952,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         // the next iteration's next-step actions, then its hand-off loads
         nrow = arow + 1 == n_act ? 0 : arow + 1;
         anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, agent ? m : 0);
-        xo = xfer_off_load_all(xf(), k + 1 >= kPackDepth ? k + 1 - kPackDepth : 0, w, lane);
+        xo = xo2;
+        xo2 = xfer_off_load_all(xf(), k + 2 >= kPackDepth ? k + 2 - kPackDepth : 0, w, lane);
         gl = xfer_grp_load(xf(), k + 1 >= 2 ? k - 1 : 0, w, lane);
         wave_sync();
     }
     // the tail: the group sums of the last two steps, then the edges of the
-    // last four (the first tail iteration's loads were issued by the loop)
+    // last five (the first two tail iterations' offset loads and the first's
+    // group load were issued by the loop)
     const int fin = cur;   // positions after the last step
     const int last_cnt = cnt_m1;
     const uint32_t last_row = row_m1;
     for (int k = K; k < K + kPackDepth; ++k) {
         if (k > K) {
-            xo = xfer_off_load_all(xf(), k >= kPackDepth ? k - kPackDepth : 0, w, lane);
+            xo = k == K + 1 ? xo2 : xfer_off_load_all(xf(), k >= kPackDepth ? k - kPackDepth : 0, w, lane);
             gl = xfer_grp_load(xf(), k >= 2 ? k - 2 : 0, w, lane);
         }
         if (k - 2 >= 0 && k - 2 < K && glast) xfer_grp_publish(xf(), gl, k - 2, w, lane, cnt_m2);
         if (k >= kPackDepth)
-            emit(k - kPackDepth, ring(cur + 2), row_m4, xfer_off_settle(xf(), xo, k - kPackDepth, w, lane));
+            emit(k - kPackDepth, ring(cur + 2), row_m5, xfer_off_settle(xf(), xo, k - kPackDepth, w, lane));
+        row_m5 = row_m4;
         row_m4 = row_m3;
         row_m3 = row_m2;
         row_m2 = row_m1;

@@ -8,8 +8,8 @@
 #        which: h c2 c3 c4 n6 n12 buffer (rollouts), h_step c4_step h_lag c4_lag
 #   bash tools/gpu.sh prof TAG [line ...]          rocprofv3 --kernel-trace --stats of bench lines
 #   bash tools/gpu.sh package TAG                  pmc (all) + tests + lines (all) + prof (h c4 eager policy buffer)
-#   bash tools/gpu.sh ab TAG variant ...           same-box A/B: bench lines h / driver / c4 of the library
-#        and of lib/ablate/VARIANT.so builds (tools/build_variant.sh), alternated twice
+#   bash tools/gpu.sh ab TAG variant ...           same-box A/B: bench lines h / driver / c4 (AB_LINES) of the
+#        library and of lib/ablate/VARIANT.so builds (tools/build_variant.sh), alternated twice
 #   bash tools/gpu.sh envsweep TAG LINE VAR v1 v2 ...   one bench line under VAR=v (e.g. GSM_ROLL_DEPTH)
 #   bash tools/gpu.sh stamps TAG which ...         phase stamps of the lib/ablate/stamps.so build
 #        which: h (launch timeline) c2 c3 c4 (tools/stamps_*.py)
@@ -112,7 +112,7 @@ case $CMD in
     for rep in 1 2; do
       for v in lib "$@"; do
         L=""; [ "$v" = lib ] || L=gs-marl_amd/gsmarl_amd/lib/ablate/$v.so
-        for l in driver h c4; do
+        for l in ${AB_LINES:-driver h c4}; do
           a=$(line_args $l) || exit 9
           GSM_LIB_PATH=$L timeout -k 10 300 python3 bench.py $a --no-cpu-baseline > $O/${l}_${v}_$rep.json 2> $O/${l}_${v}_$rep.err || { tail -20 $O/${l}_${v}_$rep.err; exit 4; }
           show "$v/$l/$rep" $O/${l}_${v}_$rep.json
