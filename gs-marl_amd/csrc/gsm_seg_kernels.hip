@@ -1966,7 +1966,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     for (int k = K; k < K + kPackDepth; ++k) {
         if (k > K) {
             xo = k == K + 1 ? xo2 : xfer_off_load_all(xf(), k >= kPackDepth ? k - kPackDepth : 0, w, lane);
-            gl = xfer_grp_load(xf(), k >= 2 ? k - 2 : 0, w, lane);
+            // (clamped to a step of this launch: the load is unconditional, and
+            // past the last step it would read beyond the granule allocation)
+            gl = xfer_grp_load(xf(), min(max(k - 2, 0), K - 1), w, lane);
         }
         if (k - 2 >= 0 && k - 2 < K && glast) xfer_grp_publish(xf(), gl, k - 2, w, lane, cnt_m2);
         if (k >= kPackDepth)
