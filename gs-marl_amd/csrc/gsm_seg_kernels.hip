@@ -1778,24 +1778,31 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         const EdgeSink out = roll_edge_sink<kSlots>(qs, j, K);
         const float2 *sp = pos_buf(pb);
         const int32_t g0 = (int32_t)(eb * E);
+        // every column's position read up front (M independent LDS reads in
+        // flight at once), then the row's edges in column order from
+        // registers: no LDS read waited on inside the per-edge chain (one
+        // wave per SIMD here: nothing else hides those latencies)
+        float2 qc[M];
+#pragma unroll
+        for (int cc = 0; cc < M; ++cc) qc[cc] = sp[cc < N ? cc : N + cc];
+        const float2 gq = sp[N + (m < N ? m : 0)];
         if (live) {
             int64_t o = env_off + (incl - c) + (m >= N ? N : 0);
             const float2 a = sp[ent];
-            auto put = [&](int64_t at, int dst) {
+            auto put = [&](int64_t at, int dst, float2 qd) {
                 if (at < out.cap) {
-                    const float2 qd = sp[dst];
                     const float dx = a.x - qd.x, dy = a.y - qd.y;
                     out.index[at] = g0 + ent;
                     out.index[out.cap + at] = g0 + dst;
                     out.attr[at] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
                 }
             };
-            constexpr uint32_t amask = (1u << N) - 1u;
-            for (uint32_t bits = row & amask; bits; bits &= bits - 1u) put(o++, __builtin_ctz(bits));
+#pragma unroll
+            for (int cc = 0; cc < N; ++cc)
+                if ((row >> cc) & 1u) put(o++, cc, qc[cc]);
             if (agent) {
-                put(o++, N + m);                                     // agent m -> its goal
-                const float2 g = sp[N + m];
-                const float dx = g.x - a.x, dy = g.y - a.y;
+                put(o++, N + m, gq);                                 // agent m -> its goal
+                const float dx = gq.x - a.x, dy = gq.y - a.y;
                 const int64_t at = env_off + a_total + m;            // goal row: goal m -> agent m
                 if (at < out.cap) {
                     out.index[at] = g0 + N + m;
@@ -1803,7 +1810,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                     out.attr[at] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
                 }
             }
-            for (uint32_t bits = row & ~amask; bits; bits &= bits - 1u) put(o++, N + __builtin_ctz(bits));
+#pragma unroll
+            for (int cc = N; cc < M; ++cc)
+                if ((row >> cc) & 1u) put(o++, N + cc, qc[cc]);
         }
         GSM_ACC(late_params(), wid, 4, te2);   // diagnostic builds: emission
     };
