@@ -8,12 +8,16 @@ owns 8192 envs with global Philox env ids, BASELINE configs[4] at N=8).
 A "step" = one env.step of every env on the GPU: action force, pairwise
 contact physics, integration, reward, collision cost, done/auto-reset, node
 features and the packed COO edge list; every observation output of every step
-is written to HBM. Inside a graph the headline (one env per
-wave) and the tile configs (C3) run all steps of the episode graph in ONE
-fused rollout launch (GSM_GRAPH_ROLL: env state kept on chip, the CSR prefix
-handed between workgroups in-launch), the other segmented configs one launch
-per step (step j+1's kernel first emits step j's edges); `--no-roll` /
-`--unfused` select those chains instead. Actions are pre-generated on device
+is written to HBM. Inside a graph every BASELINE config runs
+all steps of the episode graph in ONE fused rollout launch (GSM_GRAPH_ROLL:
+env state kept on chip, the CSR prefix handed between workgroups in-launch;
+the headline and N = 6 / 12 one env per wave, C2 four envs per wave, C3 one
+workgroup per env, C4 the ragged rollout); other shapes run one launch per
+step (step j+1's kernel first emits step j's edges); `--no-roll` /
+`--unfused` select those chains instead. `--eager` times env.step calls,
+`--policy` / `--policy-graph` a closed loop with a trivial policy (eager, or
+policy + step captured in one torch CUDA graph), `--buffer` the rollout
+buffer (every step into its own slot). Actions are pre-generated on device
 (100 x B x N int32, uniform over the 5 discrete actions) so the timed region
 has no host work; the K timed steps are replayed from HIP graphs of one
 episode (100 steps) each, with the per-episode RCCL all-reduce of episode
