@@ -1269,12 +1269,8 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         if (wave == 0) {
             KernargParams &qe = late_params();
             const int64_t kb = (int64_t)(k - 1) * gridDim.x;
-#if GSM_ABL_HANDOFF   // ablation builds only (wrong offsets): the step without the look-back
-            const int ex = 0;
-#else
             const int ex = roll_lookback(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
                                          etag | (uint32_t)k, qe.roll.status, L.lane);
-#endif
             if (L.lane == 0) {
                 s_red[0] = ex;
                 __hip_atomic_store((gu64 *)(qe.roll.gran + (int64_t)K * gridDim.x + kb + blockIdx.x),
@@ -1285,9 +1281,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         }
         GSM_ACC(p, L.b, 12, te1);   // look-back (wave 0)
         GSM_TNOW(te2);
-#if GSM_ABL_HANDOFF < 2
         __syncthreads();
-#endif
         GSM_ACC(p, L.b, 13, te2);   // waiting for it
         GSM_TNOW(te3);
         if (k == K) GSM_RSTAMP(p, L.b, 6);
@@ -1477,9 +1471,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         if (L.lane == 0) s_bc[par * kWavesPerBlock + wave] = wave_edges;
         GSM_ACC(p, L.b, 10, tw0);   // the step's work
         GSM_TNOW(tw1);
-#if GSM_ABL_HANDOFF < 2
         __syncthreads();
-#endif
         GSM_ACC(p, L.b, 11, tw1);   // the publish barrier
         if (threadIdx.x == 0) {
             int sum = 0;
