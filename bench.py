@@ -724,6 +724,20 @@ def run_rank(args):
     # nodes on the launch stream) around L back-to-back launches of that
     # kernel alone, after the timed region. Event nodes between kernels would
     # add their own packet time to every launch.
+    # Where a graph's time goes (outside the timed region): one more replay
+    # of the timed graph right after it, HIP events on its stream around the
+    # launch — the device time of a K-step graph — against K x the settled
+    # per-step time of back-to-back launches (the roofline's timing below)
+    graph_us = None
+    if not eager and not stub:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        sync()
+        e0.record()
+        run_steps(chunk, 0)
+        e1.record()
+        sync()
+        graph_us = e0.elapsed_time(e1) * 1e3
+
     roofline = None
     if not args.no_kernel_timing and not eager and not stub:
         roofline = kernel_roofline(env, cfg, actions, args, N, B, EL, roll, buf)
@@ -767,7 +781,9 @@ def run_rank(args):
                              "settle_steps": settle_steps,
                              "episode_boundaries": boundaries_in(P, K, EL),
                              "rank_ms_per_step_max": round(max(times) / K * 1e3, 5),
-                             "rank_ms_per_step_min": round(min(times) / K * 1e3, 5)},
+                             "rank_ms_per_step_min": round(min(times) / K * 1e3, 5),
+                             **graph_breakdown(graph_us, roofline, chunk, n_chunks + (1 if rem else 0),
+                                               elapsed, roll, buf is not None)},
             "episode_metrics": {"envs": gb, "finished_episodes": int(episodes),
                                 "mean_last_episode_reward": round(ep_rew / gb, 4),
                                 "mean_last_episode_cost": round(ep_cost / gb, 4),
@@ -785,6 +801,25 @@ def run_rank(args):
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def graph_breakdown(graph_us, roofline, chunk, n_graphs, elapsed, roll, buffer):
+    """Split of the timed region per graph (rank 0): `graph_device_us` = HIP
+    events around one more replay of the timed graph right after the region
+    (device time of a `chunk`-step graph); `settled_us` = chunk x the settled
+    per-step time of back-to-back launches (the roofline's timing); `fill_us`
+    = their difference, the graph's start and drain beyond its steps;
+    `host_us` = wall time per graph in the region beyond the device time
+    (launch call, synchronisation)."""
+    if graph_us is None:
+        return {}
+    out = {"graph_steps": chunk, "graph_device_us": round(graph_us, 2),
+           "host_us": round(elapsed / n_graphs * 1e6 - graph_us, 2)}
+    step_us = (roofline or {}).get("mean_launch_us")
+    if roll and step_us and not buffer:
+        out["settled_us"] = round(chunk * step_us, 2)
+        out["fill_us"] = round(graph_us - chunk * step_us, 2)
+    return out
 
 
 def counter_bound(pmc, ms, hbm_frac):

@@ -42,6 +42,12 @@ struct gsm_handle {
         int kern = 0;
         bool each = false;
         uint64_t *gran = nullptr;     // fused rollout: epoch word, then the edge-sum granules
+        // one-env-per-wave segmented rollout: the pace counters, two halves
+        // of kPaceKeys x kPaceStride words inside gran (nullptr: pacing off);
+        // a launch uses half (launches & 1) and zeroes the other for the next
+        uint32_t *pace = nullptr;
+        uint32_t launches = 0;
+        uint32_t last_epoch = 0xffffffffu;   // the epoch of the slot's previous launch
         bool roll = false;            // the graph is one rollout launch
         // A rollout graph without timing events is one kernel node: launched
         // directly (the same kernel, grid and arguments) — a plain dispatch
@@ -62,6 +68,8 @@ struct gsm_handle {
     // another stream first wait for it (gsm_graph_launch)
     hipStream_t roll_stream = nullptr;
     bool roll_launched = false;
+    hipEvent_t roll_done = nullptr;   // recorded behind every rollout-slot launch
+    uint32_t eager_last_epoch = 0xffffffffu;   // the eager one-launch step's previous epoch
     // gsm_step as a one-step rollout launch (step + its edges in one kernel):
     // -1 not yet decided for this config, 0 no (two launches), 1 yes
     int eager_roll = -1;
@@ -379,6 +387,15 @@ int redirect(gsm_handle *h, gsm::DevParams *p, const gsm_outputs *o) {
 
 uint32_t next_launch_epoch();
 hipError_t clear_status(gsm_handle *h);
+// a launch epoch other than `last` (the previous launch of the same granules:
+// the process-wide counter wraps after 2^20 launches, and an idle slot's
+// granules still carry its last launch's tags), recorded as the new last
+uint32_t fresh_epoch(uint32_t &last) {
+    uint32_t e = next_launch_epoch();
+    if (e == last) e = next_launch_epoch();
+    last = e;
+    return e;
+}
 
 // The rollout granules (in-launch hand-off words, gsm_device.h) are allocated
 // uncached: an agent-scope load of a granule line that this XCD's L2 still
@@ -429,6 +446,8 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
         if ((int64_t)per_cu * n_cu < nb) return kEagerIneligible;
         // (look-back: aggregates + inclusive prefixes per workgroup; packed
         // small envs: per-wave counts + group sums)
+        // (look-back: aggregates + inclusive prefixes per workgroup; packed
+        // small envs: per-wave counts + group sums)
         const size_t xw = (size_t)nb * gsm::kWavesPerBlock;
         const size_t bytes = 16 + std::max(2 * (size_t)nb, xw + (xw + gsm::kWave - 1) / gsm::kWave) * sizeof(uint64_t);
         e = gran_malloc((void **)&h->eager_gran, bytes);
@@ -447,8 +466,10 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
     p.ro = gsm::DevParams::RollOut{p.node_feat, p.reward, p.cost, p.done, p.edge_count, p.edge_ptr, p.edge_index,
                                    p.edge_attr, 0, 0, 0, 0, 0, 0, 0, p.edge_capacity, nullptr, nullptr, p.assign, 0};
     const int xW = nb * gsm::kWavesPerBlock, xNG = (xW + gsm::kWave - 1) / gsm::kWave;
+    // (one step: no pacing)
     p.roll = gsm::DevParams::Roll{(const char *)p.actions, 0, 1, 0, 1, xW, xNG, 0, 0, 0, h->eager_gran + 2,
-                                  h->roll_status, next_launch_epoch(), 0, nullptr, nullptr, 0, 0};
+                                  h->roll_status, fresh_epoch(h->eager_last_epoch), 0, nullptr, nullptr, 0, 0,
+                                  nullptr, nullptr};
     void *args[] = {&p};
     const hipError_t e = hipLaunchKernel(fn, dim3(nb), dim3(gsm::block_threads(p)), args, (unsigned)lds, s);
     if (e != hipSuccess) return hip_fail(h, e, "hipLaunchKernel (one-step rollout)");
@@ -486,6 +507,8 @@ void drop_slot(gsm_handle::Slot &s) {
     for (hipEvent_t ev : s.events) (void)hipEventDestroy(ev);
     if (s.gran) (void)hipFree(s.gran);
     s.gran = nullptr;
+    s.pace = nullptr;
+    s.launches = 0;
     s.roll = false;
     s.direct = false;
     s.fn = nullptr;
@@ -867,12 +890,17 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     gsm_handle::Slot &sl = h->slots[slot];
     drop_slot(sl);
     // a 16-byte header (unused), then 8-byte granules. Ragged and packed
-    // small envs: per-wave counts [K][xW] and group sums [K][xNG]; others:
-    // aggregates [K][nb] and inclusive prefixes [K][nb] (look-back). Zeroed
-    // once here — granules are tagged with the launch epoch, so replays never
-    // clear them
+    // small envs: per-wave counts [K][xW] and group sums [K][xNG]; the tile
+    // path: aggregates [K][nb] and inclusive prefixes [K][nb] (look-back); the
+    // other segmented shapes: the same, then two halves of pace counters
+    // (gsm_seg_kernels.hip pace_level). Zeroed once here — granules are
+    // tagged with the launch epoch, so replays never clear them; the untagged
+    // counters are zeroed by the launch before the one that uses them
     // (ragged: then the placement words, gsm::PlaceArea)
+    const bool paced = !tile && !per_wave;
+    const size_t pace_words = paced ? (size_t)gsm::kPaceKeys * gsm::kPaceStride : 0;   // u32, per half
     const size_t gran_alloc = 16 + (size_t)K * (per_wave ? (size_t)(xW + xNG) : 2 * (size_t)nb) * sizeof(uint64_t) +
+                              2 * pace_words * sizeof(uint32_t) +
                               (ragged ? gsm::PlaceArea::words(xW) * sizeof(uint64_t) : 0);
     e = gran_malloc((void **)&sl.gran, gran_alloc);
     if (e != hipSuccess) {
@@ -888,6 +916,11 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     e = gsm::launch_granule_init(sl.gran, gran_alloc, 0u, h->cap_stream);
     if (e == hipSuccess) e = hipStreamSynchronize(h->cap_stream);
     if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "rollout granule init"); }
+    // pacing: the rank offset in quarter steps (GSM_ROLL_PACE, default 2;
+    // 0 = no pacing: an A/B knob, outputs are the same either way)
+    int pace_q = 2;
+    if (const char *ev = getenv("GSM_ROLL_PACE")) pace_q = std::max(0, atoi(ev));
+    sl.pace = paced && pace_q > 0 ? (uint32_t *)(sl.gran + 2 + (size_t)K * 2 * nb) : nullptr;
     const bool ends = (flags & GSM_GRAPH_TIME_ENDS) != 0;
     sl.events.resize(ends ? 2 : 0, nullptr);
     for (auto &ev : sl.events) {
@@ -927,7 +960,7 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     }
     p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, xW, xNG, depth,
                                   h->sz.max_edges_per_env, place_R, sl.gran + 2, h->roll_status, 0u, place_force,
-                                  (int32_t *)h->slab, place_R ? h->place_order : nullptr, place_S, 0};
+                                  (int32_t *)h->slab, place_R ? h->place_order : nullptr, place_S, pace_q};
     if (e == hipSuccess) {
         what = "rollout kernel node";
         hipKernelNodeParams kp = {};
@@ -1155,20 +1188,46 @@ int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream) {
     if (sl.direct) {   // a rollout graph: its one kernel, launched directly
         // (GSM_GRAPH_TIME_ENDS: events recorded on the stream around it — as
         // graph event nodes they added ≈7% to the launch they bracketed)
-        hipError_t e = hipSuccess;
+        hipStream_t st = as_stream(stream);
+        // Every launch takes its own epoch and its half of the slot's double
+        // buffers, set in the arguments here: a launch captured into the
+        // caller's graph would replay one of each every time (stale granules
+        // matching its tags, unzeroed chunk sums)
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        hipError_t e = hipStreamIsCapturing(st, &cs);
+        if (e != hipSuccess) return hip_fail(h, e, "hipStreamIsCapturing");
+        if (cs != hipStreamCaptureStatusNone)
+            return fail(h, GSM_ESTATE, "a rollout graph cannot be launched into a stream capture (every launch "
+                                       "takes its own hand-off epoch); capture the per-step chain instead");
+        if (!h->roll_done) {
+            e = hipEventCreateWithFlags(&h->roll_done, hipEventDisableTiming);
+            if (e != hipSuccess) { h->roll_done = nullptr; return hip_fail(h, e, "hipEventCreate (rollout)"); }
+        }
         // rollout launches of one handle never overlap: they share its
-        // scratch and state (a launch on another stream first waits for the
-        // previous stream's work)
-        if (h->roll_launched && h->roll_stream != as_stream(stream)) e = hipStreamSynchronize(h->roll_stream);
-        if (e != hipSuccess) return hip_fail(h, e, "hipStreamSynchronize (previous rollout stream)");
-        h->roll_stream = as_stream(stream);
-        h->roll_launched = true;
-        sl.args.roll.epoch = next_launch_epoch();   // copied with the arguments at the launch
+        // scratch and state, so a launch on another stream than the previous
+        // one waits for it, asynchronously (an event recorded behind every
+        // launch: nothing here depends on the previous stream still existing)
+        if (h->roll_launched && h->roll_stream != st) {
+            e = hipStreamWaitEvent(st, h->roll_done, 0);
+            if (e != hipSuccess) return hip_fail(h, e, "hipStreamWaitEvent (previous rollout launch)");
+        }
+        sl.args.roll.epoch = fresh_epoch(sl.last_epoch);   // copied with the arguments at the launch
+        if (sl.pace) {
+            const size_t half = (size_t)gsm::kPaceKeys * gsm::kPaceStride;
+            const int par = (int)(sl.launches & 1u);
+            sl.args.roll.pace = sl.pace + par * half;
+            sl.args.roll.pace_next = sl.pace + (1 - par) * half;
+        }
         void *args[] = {&sl.args};
-        e = sl.events.empty() ? hipSuccess : hipEventRecord(sl.events.front(), as_stream(stream));
-        if (e == hipSuccess) e = hipLaunchKernel(sl.fn, sl.grid, sl.block, args, sl.lds, as_stream(stream));
-        if (e == hipSuccess && !sl.events.empty()) e = hipEventRecord(sl.events.back(), as_stream(stream));
+        e = sl.events.empty() ? hipSuccess : hipEventRecord(sl.events.front(), st);
+        if (e == hipSuccess) e = hipLaunchKernel(sl.fn, sl.grid, sl.block, args, sl.lds, st);
         if (e != hipSuccess) return hip_fail(h, e, "hipLaunchKernel (rollout)");
+        sl.launches++;
+        h->roll_stream = st;
+        h->roll_launched = true;
+        e = sl.events.empty() ? hipSuccess : hipEventRecord(sl.events.back(), st);
+        if (e == hipSuccess) e = hipEventRecord(h->roll_done, st);
+        if (e != hipSuccess) return hip_fail(h, e, "hipEventRecord (rollout)");
         return GSM_OK;
     }
     const hipError_t e = hipGraphLaunch(sl.exec, as_stream(stream));
@@ -1268,6 +1327,7 @@ int gsm_destroy(gsm_handle *h) {
     if (h->block_order) (void)hipFree(h->block_order);
     if (h->order_host) (void)hipHostFree(h->order_host);
     if (h->order_copied) (void)hipEventDestroy(h->order_copied);
+    if (h->roll_done) (void)hipEventDestroy(h->roll_done);
     delete h;
     return GSM_OK;
 }

@@ -30,6 +30,9 @@ constexpr int kMaxSegEnvsPerWave = 4;
 // gsm_device.h roll_epoch_tag)
 // (step field 4095 tags the ragged rollout's placement words, PlaceArea)
 constexpr int kRollMaxSteps = 4094;
+// pacing counters of the segmented rollout: one per CU, keyed by 11 bits of
+// XCC_ID / HW_ID (XCC, shader engine, shader array, CU), one per 64 bytes
+constexpr int kPaceKeys = 2048, kPaceStride = 16;   // counters, u32 words between them
 
 // Everything a launch needs, passed by value (kernarg segment, < 4 KB).
 // fp32 constants are formed on the host exactly as oracle/batch_ref.py:Spec
@@ -118,7 +121,14 @@ struct DevParams {
         int32_t place_force;  // test knob (GSM_ROLL_PLACE=2): register, then decide identity
         int32_t *slab;        // ragged rollout: [depth + 1][B] slabs of [slab_e + 1] u32 row-pair words + [slab_e + 1] f32
         const int32_t *place; // ragged rollout: [W] envs by descending cost (nullptr: env = wave index)
-        int32_t place_S, pad; // SIMDs the grid fills (place_R * place_S = W)
+        int32_t place_S;      // SIMDs the grid fills (place_R * place_S = W)
+        // pacing of the one-env-per-wave segmented rollout (gsm_seg_kernels.hip
+        // pace_level): the rank offset between a CU's workgroups in quarter
+        // steps, and per-CU {workgroups arrived, steps finished} counters
+        // [kPaceKeys] of this launch and of the slot's next (zeroed by this
+        // one); pace nullptr: off
+        int32_t pace_q;
+        uint32_t *pace, *pace_next;
     } roll;
     // A rollout's per-step outputs: step k's at base + k * stride (elements;
     // stride 0 = every step into the bound buffers, > 0 = a rollout buffer's

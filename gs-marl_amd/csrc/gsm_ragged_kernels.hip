@@ -1213,7 +1213,8 @@ __device__ __forceinline__ int ragged_expand(const Params &p, const RShape &s, i
             const int c = ffbl_or_neg(wd);
             const uint32_t none = (uint32_t)(c >> 31);   // all ones once the row is exhausted
             wd &= wd - 1u;
-            put((none & spare) | (~none & o), src, rowbase + (uint32_t)c);
+            // (an exhausted row's lane writes the spare word, from a valid row)
+            put((none & spare) | (~none & o), src, rowbase + ((uint32_t)c & ~none));
             o += 1u + none;
         }
     };

@@ -1161,6 +1161,46 @@ __device__ __forceinline__ float2 roll_force(const Params &p, float4 a, bool age
     return agent ? make_float2(ux * p.sens, uy * p.sens) : make_float2(0.0f, 0.0f);
 }
 
+// Pacing (round 5). A SIMD issues its ready waves oldest first below the
+// user priority (s_setprio), and a CU holds eight workgroups of the rollout,
+// dispatched one residency rank at a time (blockIdx / 256 at H). Measured per
+// CU, the rank-0 workgroup finished a 20-step launch at 109 us and rank 7 at
+// 210 us, in exact rank order on every CU, and the same without any hand-off
+// (profiles/r5_pace): the last ranks' final steps run on a CU already half
+// empty. Some order between ranks helps the look-back — a workgroup finds
+// the inclusive prefixes of the rank before it already published — but not
+// twelve steps of it. So each workgroup counts its finished steps into its
+// CU's counter (one atomic add per step, the counter loaded back beside the
+// next step's look-back loads; its rank = the arrivals before its own, read
+// at entry) and sets its waves' priority from its own
+// steps against a target: the CU's mean plus (c - rank) x q / 4 steps,
+// c = (arrivals - 1) / 2 — ahead of the target by half a step or more 0,
+// behind by as much 2, else 1. Priority only orders issue: outputs are
+// unchanged. A counter is one 32-bit word: arrivals in the top 8 bits, steps
+// in the low 24 (8 workgroups x 4094 steps < 2^24).
+constexpr uint32_t kPaceArrive = 1u << 24;
+__device__ __forceinline__ uint32_t pace_key() {
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);          // HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;   // XCC_ID
+    return (xcc << 8 | ((hw >> 13) & 7u) << 5 | ((hw >> 12) & 1u) << 4 | ((hw >> 8) & 15u)) * kPaceStride;
+}
+// the level from the CU counter as loaded after this workgroup's `done`-th
+// step was added to it
+__device__ __forceinline__ int pace_level(uint32_t fv, int done, int rank, int q) {
+    const int arr = (int)(fv >> 24), tot = (int)(fv & (kPaceArrive - 1));
+    // 8 x arrivals x (own steps - the CU's mean - (c - rank) x q / 4)
+    const int x = 8 * (done * arr - tot) - arr * (arr - 1 - 2 * rank) * q;
+    return x >= 4 * arr ? 0 : x <= -4 * arr ? 2 : 1;
+}
+__device__ __forceinline__ void pace_set(int lvl) {   // lvl wave-uniform
+    if (lvl == 0)
+        __builtin_amdgcn_s_setprio(0);
+    else if (lvl == 1)
+        __builtin_amdgcn_s_setprio(1);
+    else
+        __builtin_amdgcn_s_setprio(2);
+}
+
 // LDS per wave of the segmented rollout: [positions E | staging scratch 28 E]
 // rounded to 16 B, then [positions E | next forces N]
 constexpr int roll_lds_step(int E) { return (36 * E + 15) & ~15; }
@@ -1201,12 +1241,28 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     float2 *s_force = s_buf1 + E;
     auto pos_buf = [&](int k) { return (float2 *)(wave_lds + (k & 1) * kStep); };   // positions before step k
     int *s_bc = (int *)(smem + kWavesPerBlock * wstride);   // [2][waves]: per-env edge counts by parity
-    int *s_red = s_bc + 2 * kWavesPerBlock;                 // [2]: the workgroup's offset (+ pad)
-    int *s_pre = s_red + 2;                                 // [2][waves]: exclusive prefix of the counts
+    int *s_red = s_bc + 2 * kWavesPerBlock;                 // [4]: the workgroup's offset, pace level, rank, pad
+    int *s_pre = s_red + 4;                                 // [2][waves]: exclusive prefix of the counts
     constexpr int scr_cap = (kStep - 8 * E) / 4;
     const bool wave_live = L0.b < p.B;
     const int64_t eb = wave_live ? L0.b : 0;
     GSM_RSTAMP(p, L0.b, 0);   // diagnostic builds: the launch's timeline per wave
+    GSM_SET(p, L0.b, 9, (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |                  // HW_ID
+                            ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32));   // XCC_ID
+    // pacing: this workgroup's CU counter (the arrival now, a step after each
+    // step; its address re-formed at each use, no SGPRs held across the loop),
+    // and the counters of the slot's next launch zeroed
+    auto pacing = [] { return late_params().roll.pace != nullptr; };
+    auto pace_ctr = [] { return (gu32 *)(late_params().roll.pace + pace_key()); };
+    uint32_t pace_v = 0;   // thread 0: the arrivals before its own
+    if (pacing()) {
+        KernargParams &qz = late_params();
+        for (int i = blockIdx.x * kBlock + threadIdx.x; i < kPaceKeys; i += gridDim.x * kBlock)
+            __hip_atomic_store((gu32 *)(qz.roll.pace_next + i * kPaceStride), 0u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0)
+            pace_v = __hip_atomic_fetch_add(pace_ctr(), kPaceArrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 
     // ---- the state before step t_first and step t_first's actions
     // (p.actions); the edges of that state were emitted by whatever ran before
@@ -1219,6 +1275,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         if (L0.lane < E) s_buf0[L0.lane] = s_buf1[L0.lane] = in.x0;
         if (L0.lane + kWave < E) s_buf0[L0.lane + kWave] = s_buf1[L0.lane + kWave] = in.x1;
     }
+    if (threadIdx.x == 0) s_red[2] = (int)(pace_v >> 24);   // the rank on the CU (its load waited above)
     wave_sync();
     GSM_RSTAMP(p, L0.b, 1);
     // apply_environment_force: the action force plus the contact terms of the
@@ -1265,14 +1322,18 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         GSM_ACC(p, L.b, 14, te0);   // diagnostic builds: staging (emission, below, adds to it)
         GSM_TNOW(te1);
         // wave 0 walks back over the predecessors, hands the workgroup's
-        // offset to the other waves and publishes its inclusive prefix
+        // offset to the other waves (with this workgroup's last pace counter
+        // value) and publishes its inclusive prefix
         if (wave == 0) {
             KernargParams &qe = late_params();
             const int64_t kb = (int64_t)(k - 1) * gridDim.x;
+            // (the counter's load in flight with the look-back's)
+            const uint32_t pv = pacing() ? __hip_atomic_load(pace_ctr(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
             const int ex = roll_lookback(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
                                          etag | (uint32_t)k, qe.roll.status, L.lane);
             if (L.lane == 0) {
                 s_red[0] = ex;
+                s_red[1] = (int)pv;
                 __hip_atomic_store((gu64 *)(qe.roll.gran + (int64_t)K * gridDim.x + kb + blockIdx.x),
                                    ((uint64_t)(etag | (uint32_t)k) << 32) |
                                        (uint32_t)(ex + cb[0] + cb[1] + cb[2] + cb[3]),
@@ -1285,6 +1346,9 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         GSM_ACC(p, L.b, 13, te2);   // waiting for it
         GSM_TNOW(te3);
         if (k == K) GSM_RSTAMP(p, L.b, 6);
+        if (k < K && pacing())
+            pace_set(pace_level((uint32_t)__builtin_amdgcn_readfirstlane(s_red[1]), k,
+                                __builtin_amdgcn_readfirstlane(s_red[2]), late_params().roll.pace_q));
         // (the prefix formed once by thread 0, not w < wave selects: those
         // are loop-invariant lane masks the compiler holds in SGPR pairs)
         const int before = s_pre[(1 - par) * kWavesPerBlock + wave];
@@ -1508,6 +1572,10 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         }
         if (k == K - 1) GSM_RSTAMP(p, L.b, 4);
         if (k > 0) emit_prev(k, L);
+        // this workgroup's step into its CU's pace counter (read back in the
+        // next iteration's emission)
+        if (threadIdx.x == 0 && pacing())
+            (void)__hip_atomic_fetch_add(pace_ctr(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         // keep step t for the next iteration's emission and sweep
         oo = row;
         cand_prev = L.agent ? cand : 0ull;
@@ -2076,7 +2144,7 @@ size_t roll_kernel_lds(const DevParams &p) {
     if (p.N == n && p.No == no) return (size_t)kWavesPerBlock * pack_lds_wave<n, no>() + 4 * kWavesPerBlock;
     GSM_PACK_SHAPES(GSM_PICK)
 #undef GSM_PICK
-    return (size_t)kWavesPerBlock * roll_lds_wave(p.N, p.E) + 4 * (4 * kWavesPerBlock + 2);
+    return (size_t)kWavesPerBlock * roll_lds_wave(p.N, p.E) + 4 * (4 * kWavesPerBlock + 4);
 }
 
 const void *emit_seg_kernel_fn(const DevParams &p) {

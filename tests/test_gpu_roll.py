@@ -316,3 +316,63 @@ def test_eager_one_launch_equals_two_kernels(N, B, monkeypatch):
     for e in envs:
         assert not e.roll_gave_up()
         e.close()
+
+
+def test_roll_replay_refused_inside_stream_capture():
+    """A rollout graph takes its own hand-off epoch and its half of the chunk-
+    sum double buffer at every launch, so a launch recorded into the caller's
+    stream capture (torch.cuda.graph around env.replay) would replay one of
+    each every time: gsm_graph_launch refuses it (GSM_ESTATE) instead, and
+    the env still steps correctly afterwards."""
+    from gsmarl_amd._lib import GsmError
+    N, B, T = 24, 64, 6
+    env, _ = _env(n_agents=N, n_envs=B, episode_length=5)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    ref = _eager(env, acts, T, seed=3)
+    env.reset(seed=3)
+    env.capture(acts, T, slot=0, kernels="roll")
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream(device=DEV)
+    refused = False
+    with torch.cuda.stream(s):
+        try:
+            with torch.cuda.graph(g, stream=s):
+                try:
+                    env.replay(0)
+                except GsmError as e:
+                    refused = "stream capture" in str(e)
+        except Exception:   # an empty capture may be rejected by torch itself
+            pass
+    assert refused
+    env.replay(0)
+    torch.cuda.synchronize()
+    assert not env.roll_gave_up()
+    _same(ref, env, "roll after a refused capture")
+    env.close()
+
+
+def test_roll_replay_after_its_stream_was_destroyed():
+    """Rollout launches of one handle are ordered across streams by an event
+    recorded behind each launch (no host sync, nothing held of the previous
+    stream): a replay on a raw HIP stream that is destroyed right after, then
+    replays on torch's stream, equal eager steps."""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    N, B, T = 24, 512, 7
+    env, _ = _env(n_agents=N, n_envs=B, episode_length=5)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    ref = _eager(env, acts, 3 * T, seed=8)
+    env.reset(seed=8)
+    env.capture(acts, T, slot=0, kernels="roll")
+    torch.cuda.synchronize()
+    st = C.c_void_p()
+    assert hip.hipStreamCreate(C.byref(st)) == 0
+    env._chk(env.lib.gsm_graph_launch(env._h, 0, st), "gsm_graph_launch")
+    assert hip.hipStreamDestroy(st) == 0
+    env.replay(0)
+    env.replay(0)
+    torch.cuda.synchronize()
+    assert not env.roll_gave_up()
+    _same(ref, env, "roll across streams")
+    env.close()

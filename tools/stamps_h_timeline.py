@@ -69,5 +69,27 @@ PH = ["work", "publish_barrier", "lookback", "lookback_wait", "stage_emit"]
 res[f"replay_K{K}"] = {"events_us": e0.elapsed_time(e1) * 1e3, "marks_us": timeline(),
                        "wave0_cycles_per_step": {n: float(qq[w0, 10 + i].mean() / K) for i, n in enumerate(PH)},
                        "other_waves_cycles_per_step": {n: float(qq[~w0, 10 + i].mean() / K) for i, n in enumerate(PH)}}
+hw = qq[:, 9]
+if hw.any():
+    # where each wave ran (slot 9: HW_ID | XCC_ID << 32) against when it
+    # finished: the waves of one CU ranked by workgroup index (dispatch order)
+    cu = ((hw >> 32) & 7) << 8 | ((hw >> 13) & 7) << 5 | ((hw >> 12) & 1) << 4 | ((hw >> 8) & 15)
+    simd = cu << 2 | ((hw >> 4) & 3)
+    fin = (qq[:, 8] - qq[:, 0].min()) / 100.0
+    wg = np.arange(B) // 4
+    by_rank = {}
+    for c in np.unique(cu):
+        sel = np.nonzero(cu == c)[0]
+        wgs = np.unique(wg[sel])
+        for r, g in enumerate(wgs):
+            by_rank.setdefault(r, []).append(float(fin[sel][wg[sel] == g].max()))
+    res[f"replay_K{K}"]["finish_us_by_rank_on_cu"] = {
+        int(r): {"n": len(v), "mean": round(float(np.mean(v)), 2), "min": round(float(np.min(v)), 2),
+                 "max": round(float(np.max(v)), 2)} for r, v in sorted(by_rank.items())}
+    res[f"replay_K{K}"]["cus"] = int(len(np.unique(cu)))
+    res[f"replay_K{K}"]["simds"] = int(len(np.unique(simd)))
+    out = os.environ.get("STAMPS_NPZ")
+    if out:
+        np.savez_compressed(out, stamps=qq, hw=hw)
 print(json.dumps(res, indent=1))
 env.close()
