@@ -724,14 +724,17 @@ def run_rank(args):
     # nodes on the launch stream) around L back-to-back launches of that
     # kernel alone, after the timed region. Event nodes between kernels would
     # add their own packet time to every launch.
-    # Where a graph's time goes (outside the timed region): one more replay
-    # of the timed graph right after it, HIP events on its stream around the
-    # launch — the device time of a K-step graph — against K x the settled
-    # per-step time of back-to-back launches (the roofline's timing below)
+    # Where a graph's time goes (outside the timed region): the timed graph
+    # replayed three more times back to back (a busy GPU, as in the region),
+    # HIP events on its stream around the third — the device time of a K-step
+    # graph — against K x the settled per-step time of back-to-back launches
+    # of the roofline's timing below
     graph_us = None
     if not eager and not stub:
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         sync()
+        run_steps(chunk, 0)
+        run_steps(chunk, 0)
         e0.record()
         run_steps(chunk, 0)
         e1.record()
@@ -805,8 +808,8 @@ def run_rank(args):
 
 def graph_breakdown(graph_us, roofline, chunk, n_graphs, elapsed, roll, buffer):
     """Split of the timed region per graph (rank 0): `graph_device_us` = HIP
-    events around one more replay of the timed graph right after the region
-    (device time of a `chunk`-step graph); `settled_us` = chunk x the settled
+    events around the third of three back-to-back replays of the timed graph
+    right after the region (device time of a `chunk`-step graph); `settled_us` = chunk x the settled
     per-step time of back-to-back launches (the roofline's timing); `fill_us`
     = their difference, the graph's start and drain beyond its steps;
     `host_us` = wall time per graph in the region beyond the device time

@@ -41,10 +41,15 @@ struct gsm_handle {
         int steps = 0;
         int kern = 0;
         bool each = false;
-        uint64_t *gran = nullptr;     // fused rollout: epoch word, then the edge-sum granules
-        // one-env-per-wave segmented rollout: the pace counters, two halves
-        // of kPaceKeys x kPaceStride words inside gran (nullptr: pacing off);
-        // a launch uses half (launches & 1) and zeroes the other for the next
+        uint64_t *gran = nullptr;     // fused rollout: a 16-byte header, then the edge-sum granules
+        void *gran_base = nullptr;    // its allocation (gran_malloc: the granules end at its end)
+        // one-env-per-wave segmented rollout: the chunk sums of its one-hop
+        // CSR prefix (two halves of csum_half words inside gran) and its pace
+        // counters (two halves of kPaceKeys x kPaceStride u32; nullptr: pacing
+        // off); a launch uses half (launches & 1) and zeroes the other for the
+        // slot's next launch
+        uint64_t *csum = nullptr;
+        int64_t csum_half = 0;
         uint32_t *pace = nullptr;
         uint32_t launches = 0;
         uint32_t last_epoch = 0xffffffffu;   // the epoch of the slot's previous launch
@@ -70,10 +75,15 @@ struct gsm_handle {
     bool roll_launched = false;
     hipEvent_t roll_done = nullptr;   // recorded behind every rollout-slot launch
     uint32_t eager_last_epoch = 0xffffffffu;   // the eager one-launch step's previous epoch
+    uint64_t *eager_csum = nullptr;           // its chunk-sum halves (segmented: inside eager_gran)
+    int64_t eager_csum_half = 0;
+    uint32_t eager_launches = 0;
     // gsm_step as a one-step rollout launch (step + its edges in one kernel):
     // -1 not yet decided for this config, 0 no (two launches), 1 yes
     int eager_roll = -1;
     uint64_t *eager_gran = nullptr;   // its granules (K = 1)
+    uint64_t *eager_gran_end = nullptr;
+    void *eager_base = nullptr;       // their allocation
 };
 
 namespace {
@@ -387,6 +397,9 @@ int redirect(gsm_handle *h, gsm::DevParams *p, const gsm_outputs *o) {
 
 uint32_t next_launch_epoch();
 hipError_t clear_status(gsm_handle *h);
+// u64 words between the chunk sums of the segmented rollout's one-hop prefix
+// (gsm_device.h roll_prefix): each on a 64-byte line of its own
+constexpr int kCsumStride = 8;
 // a launch epoch other than `last` (the previous launch of the same granules:
 // the process-wide counter wraps after 2^20 launches, and an idle slot's
 // granules still carry its last launch's tags), recorded as the new last
@@ -403,11 +416,28 @@ uint32_t fresh_epoch(uint32_t &last) {
 // L2, and the hand-off then re-polls. Same box, one run each (profiles/
 // r4_gran): C2 3.44 -> 3.16 us per step, H 8.46 -> 8.31, C3 and C4 within
 // noise. GSM_GRAN_MEM = "hip" / "fine" selects hipMalloc / fine-grained (A/B).
-hipError_t gran_malloc(void **p, size_t bytes) {
+//
+// The used bytes are placed at the END of a whole number of 4 KiB pages
+// (*gran = *base + the slack): an access past the last granule leaves the
+// allocation instead of reading its own slack unnoticed (gsm_device.h
+// gran_chk; the checked build tests every address against the end).
+hipError_t gran_malloc(void **base, uint64_t **gran, size_t bytes) {
+    const size_t alloc = (bytes + 4095) & ~(size_t)4095;
     const char *ev = getenv("GSM_GRAN_MEM");
-    if (ev && !strcmp(ev, "hip")) return hipMalloc(p, bytes);
-    if (ev && !strcmp(ev, "fine")) return hipExtMallocWithFlags(p, bytes, hipDeviceMallocFinegrained);
-    return hipExtMallocWithFlags(p, bytes, hipDeviceMallocUncached);
+    hipError_t e;
+    if (ev && !strcmp(ev, "hip"))
+        e = hipMalloc(base, alloc);
+    else if (ev && !strcmp(ev, "fine"))
+        e = hipExtMallocWithFlags(base, alloc, hipDeviceMallocFinegrained);
+    else
+        e = hipExtMallocWithFlags(base, alloc, hipDeviceMallocUncached);
+    if (e != hipSuccess) {
+        *base = nullptr;
+        *gran = nullptr;
+        return e;
+    }
+    *gran = (uint64_t *)((char *)*base + (alloc - bytes));
+    return hipSuccess;
 }
 
 // gsm_step as ONE launch (opt-in, GSM_EAGER_ONE_LAUNCH=1): the config's fused
@@ -446,11 +476,18 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
         if ((int64_t)per_cu * n_cu < nb) return kEagerIneligible;
         // (look-back: aggregates + inclusive prefixes per workgroup; packed
         // small envs: per-wave counts + group sums)
-        // (look-back: aggregates + inclusive prefixes per workgroup; packed
-        // small envs: per-wave counts + group sums)
+        // (tile path: aggregates + inclusive prefixes per workgroup;
+        // segmented: aggregates + two halves of chunk sums; packed small envs:
+        // per-wave counts + group sums)
         const size_t xw = (size_t)nb * gsm::kWavesPerBlock;
-        const size_t bytes = 16 + std::max(2 * (size_t)nb, xw + (xw + gsm::kWave - 1) / gsm::kWave) * sizeof(uint64_t);
-        e = gran_malloc((void **)&h->eager_gran, bytes);
+        const size_t nc = ((size_t)nb + gsm::kPrefixChunk - 1) / gsm::kPrefixChunk;
+        const size_t words = std::max({2 * (size_t)nb, (size_t)nb + 2 * nc * kCsumStride,
+                                       xw + (xw + gsm::kWave - 1) / gsm::kWave});
+        const size_t bytes = 16 + words * sizeof(uint64_t);
+        e = gran_malloc(&h->eager_base, &h->eager_gran, bytes);
+        h->eager_gran_end = h->eager_gran ? (uint64_t *)((char *)h->eager_gran + bytes) : nullptr;
+        h->eager_csum = h->eager_gran ? h->eager_gran + 2 + nb : nullptr;
+        h->eager_csum_half = (int64_t)(nc * kCsumStride);
         if (e != hipSuccess) { h->eager_gran = nullptr; return hip_fail(h, e, "hipMalloc (eager granules)"); }
         e = gsm::launch_granule_init(h->eager_gran, bytes, 0u, nullptr);
         if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
@@ -468,8 +505,12 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
     const int xW = nb * gsm::kWavesPerBlock, xNG = (xW + gsm::kWave - 1) / gsm::kWave;
     // (one step: no pacing)
     p.roll = gsm::DevParams::Roll{(const char *)p.actions, 0, 1, 0, 1, xW, xNG, 0, 0, 0, h->eager_gran + 2,
-                                  h->roll_status, fresh_epoch(h->eager_last_epoch), 0, nullptr, nullptr, 0, 0,
-                                  nullptr, nullptr};
+                                  h->roll_status, fresh_epoch(h->eager_last_epoch)};
+    const int par = (int)(h->eager_launches++ & 1u);
+    p.roll.csum = h->eager_csum + par * h->eager_csum_half;
+    p.roll.csum_next = h->eager_csum + (1 - par) * h->eager_csum_half;
+    p.roll.csum_stride = kCsumStride;
+    p.roll.gran_end = h->eager_gran_end;
     void *args[] = {&p};
     const hipError_t e = hipLaunchKernel(fn, dim3(nb), dim3(gsm::block_threads(p)), args, (unsigned)lds, s);
     if (e != hipSuccess) return hip_fail(h, e, "hipLaunchKernel (one-step rollout)");
@@ -505,8 +546,11 @@ void drop_slot(gsm_handle::Slot &s) {
     if (s.exec) (void)hipGraphExecDestroy(s.exec);
     if (s.graph) (void)hipGraphDestroy(s.graph);
     for (hipEvent_t ev : s.events) (void)hipEventDestroy(ev);
-    if (s.gran) (void)hipFree(s.gran);
+    if (s.gran_base) (void)hipFree(s.gran_base);
+    s.gran_base = nullptr;
     s.gran = nullptr;
+    s.csum = nullptr;
+    s.csum_half = 0;
     s.pace = nullptr;
     s.launches = 0;
     s.roll = false;
@@ -863,7 +907,10 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
                 (void)hipFree(h->slab);
             }
             for (auto &o : h->slots)
-                if (o.roll && o.args.path == gsm::kPathRagged) o.args.roll.slab = (int32_t *)fresh;
+                if (o.roll && o.args.path == gsm::kPathRagged) {
+                    o.args.roll.slab = (int32_t *)fresh;
+                    o.args.roll.slab_end = (int32_t *)((char *)fresh + need);
+                }
             h->slab = fresh;
             h->slab_bytes = need;
         }
@@ -892,17 +939,26 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     // a 16-byte header (unused), then 8-byte granules. Ragged and packed
     // small envs: per-wave counts [K][xW] and group sums [K][xNG]; the tile
     // path: aggregates [K][nb] and inclusive prefixes [K][nb] (look-back); the
-    // other segmented shapes: the same, then two halves of pace counters
-    // (gsm_seg_kernels.hip pace_level). Zeroed once here — granules are
-    // tagged with the launch epoch, so replays never clear them; the untagged
-    // counters are zeroed by the launch before the one that uses them
+    // other segmented shapes (one env per wave): aggregates [K][nb], two
+    // halves of chunk sums [K][nc] kCsumStride apart (gsm_device.h
+    // roll_prefix) and two halves of pace counters (gsm_seg_kernels.hip
+    // pace_level). Zeroed once here — granules are tagged with the launch
+    // epoch, so replays never clear them; the untagged chunk sums and counters
+    // are zeroed by the launch before the one that uses them
     // (ragged: then the placement words, gsm::PlaceArea)
     const bool paced = !tile && !per_wave;
+    const size_t nc = ((size_t)nb + gsm::kPrefixChunk - 1) / gsm::kPrefixChunk;
+    if (paced && nc > (size_t)gsm::kWave) {   // roll_prefix: one chunk sum per lane
+        if (fallback) return kRollIneligible;
+        return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: more than 4096 workgroups in one rollout launch");
+    }
+    const size_t csum_half = paced ? (size_t)K * nc * kCsumStride : 0;   // u64
     const size_t pace_words = paced ? (size_t)gsm::kPaceKeys * gsm::kPaceStride : 0;   // u32, per half
-    const size_t gran_alloc = 16 + (size_t)K * (per_wave ? (size_t)(xW + xNG) : 2 * (size_t)nb) * sizeof(uint64_t) +
+    const size_t gran_alloc = 16 + ((size_t)K * (per_wave ? (size_t)(xW + xNG) : paced ? (size_t)nb : 2 * (size_t)nb) +
+                                    2 * csum_half) * sizeof(uint64_t) +
                               2 * pace_words * sizeof(uint32_t) +
                               (ragged ? gsm::PlaceArea::words(xW) * sizeof(uint64_t) : 0);
-    e = gran_malloc((void **)&sl.gran, gran_alloc);
+    e = gran_malloc(&sl.gran_base, &sl.gran, gran_alloc);
     if (e != hipSuccess) {
         sl.gran = nullptr;
         if (fallback) return kRollIneligible;   // the per-step chain needs no granules
@@ -918,9 +974,19 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     if (e != hipSuccess) { drop_slot(sl); return hip_fail(h, e, "rollout granule init"); }
     // pacing: the rank offset in quarter steps (GSM_ROLL_PACE, default 2;
     // 0 = no pacing: an A/B knob, outputs are the same either way)
-    int pace_q = 2;
-    if (const char *ev = getenv("GSM_ROLL_PACE")) pace_q = std::max(0, atoi(ev));
-    sl.pace = paced && pace_q > 0 ? (uint32_t *)(sl.gran + 2 + (size_t)K * 2 * nb) : nullptr;
+    int pace_q = 0;
+    bool pace_on = true;
+    if (const char *ev = getenv("GSM_ROLL_PACE")) {
+        if (!strcmp(ev, "off"))
+            pace_on = false;
+        else
+            pace_q = std::max(0, atoi(ev));
+    }
+    if (paced) {
+        sl.csum = sl.gran + 2 + (size_t)K * nb;
+        sl.csum_half = (int64_t)csum_half;
+        sl.pace = pace_on ? (uint32_t *)(sl.csum + 2 * csum_half) : nullptr;
+    }
     const bool ends = (flags & GSM_GRAPH_TIME_ENDS) != 0;
     sl.events.resize(ends ? 2 : 0, nullptr);
     for (auto &ev : sl.events) {
@@ -961,6 +1027,9 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     p.roll = gsm::DevParams::Roll{(const char *)actions, stride, n_actions, 0, K, xW, xNG, depth,
                                   h->sz.max_edges_per_env, place_R, sl.gran + 2, h->roll_status, 0u, place_force,
                                   (int32_t *)h->slab, place_R ? h->place_order : nullptr, place_S, pace_q};
+    p.roll.csum_stride = kCsumStride;   // (csum, pace: set per launch, gsm_graph_launch)
+    p.roll.gran_end = (uint64_t *)((char *)sl.gran + gran_alloc);
+    p.roll.slab_end = h->slab ? (int32_t *)((char *)h->slab + h->slab_bytes) : nullptr;
     if (e == hipSuccess) {
         what = "rollout kernel node";
         hipKernelNodeParams kp = {};
@@ -1022,7 +1091,7 @@ int gsm_graph_roll_status(gsm_handle *h, int32_t *gave_up) {
         if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
     }
     if (e != hipSuccess) return hip_fail(h, e, "rollout status read");
-    *gave_up = v ? 1 : 0;
+    *gave_up = (int32_t)v;   // the reason code (gsm.h), 0 if none
     return GSM_OK;
 }
 
@@ -1212,9 +1281,13 @@ int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream) {
             if (e != hipSuccess) return hip_fail(h, e, "hipStreamWaitEvent (previous rollout launch)");
         }
         sl.args.roll.epoch = fresh_epoch(sl.last_epoch);   // copied with the arguments at the launch
+        const int par = (int)(sl.launches & 1u);
+        if (sl.csum) {
+            sl.args.roll.csum = sl.csum + par * sl.csum_half;
+            sl.args.roll.csum_next = sl.csum + (1 - par) * sl.csum_half;
+        }
         if (sl.pace) {
             const size_t half = (size_t)gsm::kPaceKeys * gsm::kPaceStride;
-            const int par = (int)(sl.launches & 1u);
             sl.args.roll.pace = sl.pace + par * half;
             sl.args.roll.pace_next = sl.pace + (1 - par) * half;
         }
@@ -1322,7 +1395,7 @@ int gsm_destroy(gsm_handle *h) {
     if (h->roll_status) (void)hipFree(h->roll_status);
     if (h->edge_scratch) (void)hipFree(h->edge_scratch);
     if (h->slab) (void)hipFree(h->slab);
-    if (h->eager_gran) (void)hipFree(h->eager_gran);
+    if (h->eager_base) (void)hipFree(h->eager_base);
     if (h->order_copied) (void)hipEventSynchronize(h->order_copied);
     if (h->block_order) (void)hipFree(h->block_order);
     if (h->order_host) (void)hipHostFree(h->order_host);

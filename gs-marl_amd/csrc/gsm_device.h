@@ -240,11 +240,42 @@ typedef __attribute__((address_space(1))) uint64_t gu64;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 constexpr uint64_t kRollSpinTicks = 20000000ull;   // s_memrealtime ticks (100 MHz): 0.2 s
 
+// Every granule access of the rollouts' hand-offs goes through gran_ld /
+// gran_st (relaxed agent-scope: write-through, L1 bypassed). Several are
+// issued unconditionally at clamped addresses (a load under a branch makes
+// the compiler drain the memory counter at every later wait), so a wrong
+// clamp reads outside the allocation — once past its end into another
+// page (a GPU memory fault, round 4), once inside its page slack, unnoticed.
+// The checked build (-DGSM_CHECKED, tools/build_variant.sh; never the
+// product library) tests every such address against the slot's allocation
+// [roll.gran, roll.gran_end): one outside sets the sticky status word to
+// kStatusOutOfBounds and is redirected to the first granule, so the tests
+// (which fail on any non-zero status) name it without faulting the GPU.
+constexpr uint32_t kStatusOutOfBounds = 6u;
+#ifdef GSM_CHECKED
+__device__ __forceinline__ const uint64_t *gran_chk(const uint64_t *g) {
+    KernargParams &q = late_params();
+    if (__builtin_expect(g < q.roll.gran || g >= q.roll.gran_end, 0)) {
+        __hip_atomic_store((gu32 *)q.roll.status, kStatusOutOfBounds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return q.roll.gran;
+    }
+    return g;
+}
+#else
+__device__ __forceinline__ const uint64_t *gran_chk(const uint64_t *g) { return g; }
+#endif
+__device__ __forceinline__ uint64_t gran_ld(const uint64_t *g) {
+    return __hip_atomic_load((const gu64 *)gran_chk(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gran_st(uint64_t *g, uint64_t v) {
+    __hip_atomic_store((gu64 *)gran_chk(g), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // one granule, polled until its tag matches (cold path)
 __device__ __forceinline__ uint64_t roll_wait(const uint64_t *g, uint32_t tag, uint32_t *status) {
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     for (;;) {
-        const uint64_t x = __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t x = gran_ld(g);
         if ((uint32_t)(x >> 32) == tag) return x;
         if (__hip_atomic_load((gu32 *)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u ||
             __builtin_amdgcn_s_memrealtime() - t0 > kRollSpinTicks) {
@@ -315,12 +346,8 @@ struct Xfer {
     uint32_t etag;      // roll_epoch_tag(epoch)
     __device__ __forceinline__ uint32_t tag(int s) const { return etag | (uint32_t)(s + 1); }
 };
-__device__ __forceinline__ uint64_t xfer_ld(const uint64_t *g) {
-    return __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void xfer_st(uint64_t *g, uint32_t tag, uint32_t v) {
-    __hip_atomic_store((gu64 *)g, (uint64_t)tag << 32 | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
+__device__ __forceinline__ uint64_t xfer_ld(const uint64_t *g) { return gran_ld(g); }
+__device__ __forceinline__ void xfer_st(uint64_t *g, uint32_t tag, uint32_t v) { gran_st(g, (uint64_t)tag << 32 | v); }
 // The value of a granule loaded as x from g on lanes `act`, once its tag is
 // `tag` (re-polled until it is: the cold path); 0 on other lanes.
 __device__ __forceinline__ uint32_t xfer_settle(uint64_t x, const uint64_t *g, bool act, uint32_t tag,
@@ -381,15 +408,80 @@ __device__ __forceinline__ int xfer_off_settle(const Xfer &x, const XferOff &o, 
     return wave_total((int)v);
 }
 // Group sum of step s by the group's last wave (w & 63 == 63): the other 63
-// members' granules plus its own count.
+// members' granules plus its own count. The load is issued by every wave (a
+// load under a branch drains the memory counter at later waits); its index
+// stays inside step s's row also for a wave of a partial last group, whose
+// result is never used (the checked build caught the unclamped form reading
+// past the allocation at the last step of a 16-wave grid).
+__device__ __forceinline__ const uint64_t *xfer_grp_addr(const Xfer &x, int s, int w, int lane) {
+    return x.agg + (int64_t)s * x.W + min((w & ~63) + min(lane, 62), x.W - 1);
+}
 __device__ __forceinline__ uint64_t xfer_grp_load(const Xfer &x, int s, int w, int lane) {
-    return xfer_ld(x.agg + (int64_t)s * x.W + (w & ~63) + min(lane, 62));
+    return xfer_ld(xfer_grp_addr(x, s, w, lane));
 }
 __device__ __forceinline__ void xfer_grp_publish(const Xfer &x, uint64_t l, int s, int w, int lane, int own) {
     const uint32_t tag = x.tag(s);
-    const uint32_t v = xfer_settle(l, x.agg + (int64_t)s * x.W + (w & ~63) + min(lane, 62), lane < 63, tag, x.status);
+    const uint32_t v = xfer_settle(l, xfer_grp_addr(x, s, w, lane), lane < 63, tag, x.status);
     const int sum = wave_total((int)v) + own;
     if (lane == 0) xfer_st(x.grp + (int64_t)s * x.NG + (w >> 6), tag, (uint32_t)sum);
+}
+
+// ---- one-hop CSR prefix of the one-env-per-wave segmented rollout (round 5)
+// The packed offset of workgroup w's edges of step s is the sum of the edge
+// counts of every workgroup before it. Two kinds of words per step:
+//   agg[s][w]  workgroup w's count, a tagged granule;
+//   sum[s][c]  chunk c = workgroups [64c, 64c + 64): {arrivals32, sum32}, formed
+//              by one agent-scope atomic add (1 << 32 | count) of each member
+//              (the chunk words `cs` u64 apart: spread over memory lines).
+// offset(w) = sum[s][c'] over the chunks c' < w / 64 (each complete: arrivals
+// 64) + agg[s][w'] over w's chunk-mates w' < w: ONE load per lane and no
+// chain. (A decoupled look-back resolves through the predecessors' inclusive
+// prefixes, each published after its own walk: workgroups that reach a step
+// together wait on each other hop by hop, and only a skew of whole steps
+// between the CU's dispatch ranks hid that — DESIGN.md §4.) The rollout reads
+// a step's words two iterations after publishing them, so they are complete
+// at the first load unless a workgroup trails by two steps (then re-polled).
+// The sum words carry no tag: each launch uses one half of a double buffer
+// and zeroes the other, which the slot's next launch uses.
+__device__ __forceinline__ void prefix_publish(uint64_t *agg_s, uint64_t *sum_s, int cs, int w, uint32_t tag,
+                                               uint32_t v) {
+    gran_st(agg_s + w, (uint64_t)tag << 32 | v);
+    (void)__hip_atomic_fetch_add((gu64 *)(sum_s + (int64_t)(w / kPrefixChunk) * cs), 1ull << 32 | v,
+                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Workgroup w's exclusive prefix of step s (ONE wave; wave-uniform result).
+// Lane l loads chunk sum l (l < w / 64) and chunk-mate 64(w / 64) + l's
+// aggregate (l < w % 64), at clamped addresses inside the step's rows; a word
+// not yet complete is re-polled (bounded: kRollSpinTicks, then the sticky
+// status word and a zero contribution).
+__device__ __forceinline__ int roll_prefix(const uint64_t *agg_s, const uint64_t *sum_s, int cs, uint32_t tag,
+                                           uint32_t *status, int lane) {
+    int w = (int)blockIdx.x;
+    asm volatile("" : "+s"(w));   // no window predicates hoisted into a rollout's loop (SGPR pairs)
+    const int c = w / kPrefixChunk, r = w % kPrefixChunk;
+    const uint64_t *sp = sum_s + (int64_t)min(lane, c > 0 ? c - 1 : 0) * cs;
+    const uint64_t *ap = agg_s + c * kPrefixChunk + min(lane, r > 0 ? r - 1 : 0);
+    uint64_t sv = __hip_atomic_load((const gu64 *)sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t av = gran_ld(ap);
+    const bool use_s = lane < c, use_a = lane < r;
+    bool sb = use_s && (uint32_t)(sv >> 32) != (uint32_t)kPrefixChunk;
+    bool ab = use_a && (uint32_t)(av >> 32) != tag;
+    if (__builtin_expect(__builtin_amdgcn_ballot_w64(sb || ab) != 0, 0)) {
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        do {
+            __builtin_amdgcn_s_sleep(8);
+            if (sb) sv = __hip_atomic_load((const gu64 *)sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (ab) av = gran_ld(ap);
+            sb = use_s && (uint32_t)(sv >> 32) != (uint32_t)kPrefixChunk;
+            ab = use_a && (uint32_t)(av >> 32) != tag;
+            if (__builtin_amdgcn_s_memrealtime() - t0 > kRollSpinTicks ||
+                __hip_atomic_load((gu32 *)status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+                __hip_atomic_store((gu32 *)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                sb = ab = false;
+            }
+        } while (__builtin_amdgcn_ballot_w64(sb || ab) != 0);
+    }
+    return wave_total((int)((use_s ? (uint32_t)sv : 0u) + (use_a ? (uint32_t)av : 0u)));
 }
 
 // Decoupled look-back over the preceding workgroups (ONE wave; wave-uniform
@@ -411,8 +503,8 @@ __device__ __forceinline__ int roll_lookback(const uint64_t *agg_k, const uint64
         const int idx = hi - 1 - lane;                      // lane 0 = nearest predecessor
         const int ci = idx >= 0 ? idx : 0;
         const bool valid = idx >= 0;
-        const uint64_t xi = __hip_atomic_load((const gu64 *)(inc_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        uint64_t a = __hip_atomic_load((const gu64 *)(agg_k + ci), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t xi = gran_ld(inc_k + ci);
+        uint64_t a = gran_ld(agg_k + ci);
         const uint64_t have = __ballot(valid && (uint32_t)(xi >> 32) == tag);
         const int j = have ? __builtin_ctzll(have) : kWave;   // wave-uniform
         // aggregates of lanes < j (all valid lanes when no inclusive was found)

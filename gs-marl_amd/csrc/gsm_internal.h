@@ -33,6 +33,9 @@ constexpr int kRollMaxSteps = 4094;
 // pacing counters of the segmented rollout: one per CU, keyed by 11 bits of
 // XCC_ID / HW_ID (XCC, shader engine, shader array, CU), one per 64 bytes
 constexpr int kPaceKeys = 2048, kPaceStride = 16;   // counters, u32 words between them
+// workgroups per chunk sum of the segmented rollout's one-hop CSR prefix
+// (gsm_device.h roll_prefix)
+constexpr int kPrefixChunk = 64;
 
 // Everything a launch needs, passed by value (kernarg segment, < 4 KB).
 // fp32 constants are formed on the host exactly as oracle/batch_ref.py:Spec
@@ -129,6 +132,15 @@ struct DevParams {
         // one); pace nullptr: off
         int32_t pace_q;
         uint32_t *pace, *pace_next;
+        // the one-hop CSR prefix of that rollout (gsm_device.h roll_prefix):
+        // this launch's chunk sums [K][nc] at csum_stride u64 apart, and the
+        // other half of the slot's double buffer (zeroed by this launch)
+        uint64_t *csum, *csum_next;
+        int32_t csum_stride, pad2;
+        // one past the slot's granule words and the ragged slabs (bounds of
+        // the checked build's address tests, gsm_device.h gran_chk)
+        uint64_t *gran_end;
+        int32_t *slab_end;
     } roll;
     // A rollout's per-step outputs: step k's at base + k * stride (elements;
     // stride 0 = every step into the bound buffers, > 0 = a rollout buffer's

@@ -1297,7 +1297,7 @@ constexpr uint64_t kPlaceWaitTicks = 40000;    // 400 us of s_memrealtime
 constexpr uint64_t kPlaceStallTicks = 5000;    // 50 us without a new arrival
 constexpr uint32_t kPlaceIdentity = 1, kPlaceDealt = 2;
 __device__ __forceinline__ uint64_t place_ld(const uint64_t *g) {   // a wave-uniform atomic load
-    const uint64_t x = __hip_atomic_load((const gu64 *)g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t x = gran_ld(g);
     return (uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)) << 32 |
            __builtin_amdgcn_readfirstlane((uint32_t)x);
 }
@@ -1360,14 +1360,12 @@ __device__ int roll_place(const int wg_wave, const uint32_t epoch) {
         int seen = -1;
         uint64_t t_seen = t0;
         for (;;) {
-            const uint64_t a = __hip_atomic_load((gu64 *)(A + PlaceArea::kArrive + 8 * lane), __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t a = gran_ld(A + PlaceArea::kArrive + 8 * lane);
             const int arrived = wave_total((int)a);
             const uint64_t tn = __builtin_amdgcn_s_memrealtime();
             if (arrived == (int)gridDim.x) {
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // every registration before the reads below
-                const uint64_t n = __hip_atomic_load((gu64 *)(A + PlaceArea::kNsimd + 8 * lane), __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t n = gran_ld(A + PlaceArea::kNsimd + 8 * lane);
                 const uint64_t bad = place_ld(A + PlaceArea::kBad);
                 dec = (wave_total((int)n) == S && (uint32_t)(bad >> 32) != ptag && !q.roll.place_force)
                           ? kPlaceDealt : kPlaceIdentity;
@@ -1421,8 +1419,7 @@ __device__ int roll_place(const int wg_wave, const uint32_t epoch) {
             return wg_wave;
         }
     }
-    const uint64_t nx = lane < (int)grp ? __hip_atomic_load((gu64 *)(A + PlaceArea::kNsimd + 8 * lane),
-                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    const uint64_t nx = lane < (int)grp ? gran_ld(A + PlaceArea::kNsimd + 8 * lane) : 0ull;
     const int i = __builtin_amdgcn_readfirstlane((int)(uint32_t)rk + wave_total((int)nx));
     const int r = __popc((uint32_t)mk & ((1u << slot) - 1u));
     // a dealt slot is inside the table by construction (exactly S SIMDs, none
@@ -1518,6 +1515,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         KernargParams &q = late_params();
         const int64_t per = 2 * ((int64_t)q.roll.slab_e + 1);
         int32_t *base = q.roll.slab + ((int64_t)j * q.B + eb) * per;
+#ifdef GSM_CHECKED   // (gsm_device.h gran_chk) the env's slab inside the slab allocation
+        if (base < q.roll.slab || base + per > q.roll.slab_end) {
+            __hip_atomic_store((gu32 *)q.roll.status, kStatusOutOfBounds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            base = q.roll.slab;
+        }
+#endif
         return Slab{(uint32_t *)base, (float *)(base + q.roll.slab_e + 1)};
     };
     int ring = 0;                    // k mod (depth + 1): the slab / count of the current step
@@ -1612,6 +1615,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         }
         const Slab src = slab_of(jr);
         const EdgeSink dst = roll_edge_sink<kSlots>(q, j, K);
+#ifdef GSM_CHECKED   // the slab's words read below lie inside it
+        if (cnt > q.roll.slab_e + 1 && lane == 0)
+            __hip_atomic_store((gu32 *)q.roll.status, kStatusOutOfBounds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
         int32_t g0 = (int32_t)(eb * Emax);   // the env's first global node id
         asm volatile("" : "+v"(g0));
         for (int e = lane; e < cnt; e += kWave) {

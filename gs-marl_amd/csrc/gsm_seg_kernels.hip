@@ -1202,9 +1202,10 @@ __device__ __forceinline__ void pace_set(int lvl) {   // lvl wave-uniform
 }
 
 // LDS per wave of the segmented rollout: [positions E | staging scratch 28 E]
-// rounded to 16 B, then [positions E | next forces N]
+// rounded to 16 B, then [positions E][positions E][next forces N][row masks
+// of 64 lanes]
 constexpr int roll_lds_step(int E) { return (36 * E + 15) & ~15; }
-constexpr int roll_lds_wave(int N, int E) { return roll_lds_step(E) + 8 * E + 8 * N; }
+constexpr int roll_lds_wave(int N, int E) { return roll_lds_step(E) + 16 * E + 8 * N + 8 * kWave; }
 
 // kSlots: per-step outputs at base + k * stride (a rollout buffer); else every
 // step into the bound buffers (the strides are 0 and fold away)
@@ -1227,22 +1228,26 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     L0.live = L0.lane < M && L0.b < p.B;
     L0.agent = L0.live && L0.m < N;
     const int wave = L0.wave;
-    // Positions ping-pong between two LDS buffers: step k reads buffer k & 1
-    // and writes the agents' new positions into the other, so the previous
-    // step's positions (for its emission) need no copy; goals and obstacles
-    // (static within an episode) are kept in both. Compile-time layout
-    // (roll_kernel_lds): [positions | staging scratch], [positions | the next
-    // step's agent forces].
+    // Positions rotate through three LDS buffers: step k reads buffer k % 3
+    // and writes the agents' new positions into buffer (k + 1) % 3, so the
+    // positions after step k - 2, which iteration k emits the edges of, are
+    // still in the third; goals and obstacles (static within an episode) are
+    // kept in all three. Compile-time layout (roll_kernel_lds): [positions |
+    // staging scratch], [positions], [positions], [the next step's agent
+    // forces], [the row masks of step k - 2].
     constexpr int kStep = roll_lds_step(E), wstride = roll_lds_wave(N, E);
     unsigned char *wave_lds = smem + wave * wstride;
     float2 *const s_buf0 = (float2 *)wave_lds;
     float *s_nf = (float *)(s_buf0 + E);
     float2 *const s_buf1 = (float2 *)(wave_lds + kStep);
-    float2 *s_force = s_buf1 + E;
-    auto pos_buf = [&](int k) { return (float2 *)(wave_lds + (k & 1) * kStep); };   // positions before step k
-    int *s_bc = (int *)(smem + kWavesPerBlock * wstride);   // [2][waves]: per-env edge counts by parity
-    int *s_red = s_bc + 2 * kWavesPerBlock;                 // [4]: the workgroup's offset, pace level, rank, pad
-    int *s_pre = s_red + 4;                                 // [2][waves]: exclusive prefix of the counts
+    float2 *const s_buf2 = s_buf1 + E;
+    float2 *s_force = s_buf2 + E;
+    uint64_t *const s_row = (uint64_t *)(s_force + N);
+    // positions before step j, by j % 3
+    auto pos_buf = [&](int j3) { return (float2 *)(wave_lds + (j3 == 0 ? 0 : kStep + (j3 - 1) * 8 * E)); };
+    int *s_bc = (int *)(smem + kWavesPerBlock * wstride);   // [3][waves]: per-env edge counts by step % 3
+    int *s_red = s_bc + 3 * kWavesPerBlock;                 // [4]: the workgroup's offset, pace counter, rank, pad
+    int *s_pre = s_red + 4;                                 // [3][waves]: exclusive prefix of the counts
     constexpr int scr_cap = (kStep - 8 * E) / 4;
     const bool wave_live = L0.b < p.B;
     const int64_t eb = wave_live ? L0.b : 0;
@@ -1255,6 +1260,16 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     auto pacing = [] { return late_params().roll.pace != nullptr; };
     auto pace_ctr = [] { return (gu32 *)(late_params().roll.pace + pace_key()); };
     uint32_t pace_v = 0;   // thread 0: the arrivals before its own
+    // one-hop prefix: chunks of 64 workgroups, their sums `cs` u64 apart; the
+    // slot's next launch's chunk sums zeroed
+    const int nc = ((int)gridDim.x + kPrefixChunk - 1) / kPrefixChunk;
+    {
+        KernargParams &qz = late_params();
+        const int cs = qz.roll.csum_stride, n = qz.roll.K * nc;
+        for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
+            __hip_atomic_store((gu64 *)(qz.roll.csum_next + (int64_t)i * cs), 0ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (pacing()) {
         KernargParams &qz = late_params();
         for (int i = blockIdx.x * kBlock + threadIdx.x; i < kPaceKeys; i += gridDim.x * kBlock)
@@ -1272,8 +1287,8 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     float2 acc = in.acc, v = in.v, u = in.u;
     uint64_t cand_prev = in.cand_prev, oo = in.oo;
     if (wave_live) {
-        if (L0.lane < E) s_buf0[L0.lane] = s_buf1[L0.lane] = in.x0;
-        if (L0.lane + kWave < E) s_buf0[L0.lane + kWave] = s_buf1[L0.lane + kWave] = in.x1;
+        if (L0.lane < E) s_buf0[L0.lane] = s_buf1[L0.lane] = s_buf2[L0.lane] = in.x0;
+        if (L0.lane + kWave < E) s_buf0[L0.lane + kWave] = s_buf1[L0.lane + kWave] = s_buf2[L0.lane + kWave] = in.x1;
     }
     if (threadIdx.x == 0) s_red[2] = (int)(pace_v >> 24);   // the rank on the CU (its load waited above)
     wave_sync();
@@ -1310,48 +1325,44 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     const uint32_t etag = roll_epoch_tag(p.roll.epoch);     // this launch's tag base
     int arow = p.roll.t_first % n_act;                      // action row of the current step
     uint8_t deg = 0;                                        // App. A S16 flags of the final state
-    // The edges of step t_first + k - 1, emitted in iteration k (k = 1..K-1)
-    // and by the tail after the loop (k = K): kept positions and row masks;
-    // the counts of this workgroup's envs are read before the exchange barrier.
-    auto emit_prev = [&](const int k, const Lane &L) {
-        const int par = k & 1;
-        const int *cb = s_bc + (1 - par) * kWavesPerBlock;   // this workgroup's counts of step t - 1
+    // The edges of step t_first + j (j < K), emitted two iterations later
+    // (iteration j + 2; the last two steps' by the tail after the loop): its
+    // positions kept in buffer pj3, its row masks `mask`, this workgroup's
+    // counts of it in s_bc[cj3]. `done`: the steps this workgroup has added to
+    // its CU's pace counter (0: no pacing here, the tail).
+    auto emit_step = [&](const int j, const int pj3, const int cj3, const uint64_t mask, const int done,
+                         const Lane &L) {
+        const int *cb = s_bc + cj3 * kWavesPerBlock;   // this workgroup's counts of step j
         // the env's list staged first (needs only its own row counts)
         GSM_TNOW(te0);
-        const int staged = wave_live ? stage_rows<kN, kNo>(L, (uint32_t *)s_nf, scr_cap, oo) : -1;
+        const int staged = wave_live ? stage_rows<kN, kNo>(L, (uint32_t *)s_nf, scr_cap, mask) : -1;
         GSM_ACC(p, L.b, 14, te0);   // diagnostic builds: staging (emission, below, adds to it)
         GSM_TNOW(te1);
-        // wave 0 walks back over the predecessors, hands the workgroup's
-        // offset to the other waves (with this workgroup's last pace counter
-        // value) and publishes its inclusive prefix
+        // wave 0 forms the workgroup's offset (one hop: the chunk sums and its
+        // chunk-mates' counts, published two iterations ago) and hands it to
+        // the other waves, with its CU's pace counter loaded beside it
         if (wave == 0) {
             KernargParams &qe = late_params();
-            const int64_t kb = (int64_t)(k - 1) * gridDim.x;
-            // (the counter's load in flight with the look-back's)
-            const uint32_t pv = pacing() ? __hip_atomic_load(pace_ctr(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
-            const int ex = roll_lookback(qe.roll.gran + kb, qe.roll.gran + (int64_t)K * gridDim.x + kb,
-                                         etag | (uint32_t)k, qe.roll.status, L.lane);
+            const uint32_t pv = done > 0 ? __hip_atomic_load(pace_ctr(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
+            const int cs = qe.roll.csum_stride;
+            const int ex = roll_prefix(qe.roll.gran + (int64_t)j * gridDim.x, qe.roll.csum + (int64_t)j * nc * cs, cs,
+                                       etag | (uint32_t)(j + 1), qe.roll.status, L.lane);
             if (L.lane == 0) {
                 s_red[0] = ex;
                 s_red[1] = (int)pv;
-                __hip_atomic_store((gu64 *)(qe.roll.gran + (int64_t)K * gridDim.x + kb + blockIdx.x),
-                                   ((uint64_t)(etag | (uint32_t)k) << 32) |
-                                       (uint32_t)(ex + cb[0] + cb[1] + cb[2] + cb[3]),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
         }
-        GSM_ACC(p, L.b, 12, te1);   // look-back (wave 0)
+        GSM_ACC(p, L.b, 12, te1);   // the prefix (wave 0)
         GSM_TNOW(te2);
         __syncthreads();
         GSM_ACC(p, L.b, 13, te2);   // waiting for it
         GSM_TNOW(te3);
-        if (k == K) GSM_RSTAMP(p, L.b, 6);
-        if (k < K && pacing())
-            pace_set(pace_level((uint32_t)__builtin_amdgcn_readfirstlane(s_red[1]), k,
+        if (done > 0)
+            pace_set(pace_level((uint32_t)__builtin_amdgcn_readfirstlane(s_red[1]), done,
                                 __builtin_amdgcn_readfirstlane(s_red[2]), late_params().roll.pace_q));
         // (the prefix formed once by thread 0, not w < wave selects: those
         // are loop-invariant lane masks the compiler holds in SGPR pairs)
-        const int before = s_pre[(1 - par) * kWavesPerBlock + wave];
+        const int before = s_pre[cj3 * kWavesPerBlock + wave];
         const int my_cnt = cb[wave];
         int64_t env_off = (int64_t)s_red[0] + before;
         // (an offset past the capacity is a legal overflow of a small slot:
@@ -1364,20 +1375,22 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         if (wave_live) {
             KernargParams &qs = late_params();
             if (L.lane == 0) {
-                int64_t *const eptr = qs.ro.eptr + (kSlots ? (k - 1) * qs.ro.ep_s : 0);
+                int64_t *const eptr = qs.ro.eptr + (kSlots ? j * qs.ro.ep_s : 0);
                 eptr[L.b] = env_off;
                 if (L.b == qs.B - 1) eptr[qs.B] = env_off + my_cnt;
             }
-            const EdgeSink out = roll_edge_sink<kSlots>(qs, k - 1, K);
-            const float2 *s_prev = pos_buf(k);                  // positions after step t - 1
+            const EdgeSink out = roll_edge_sink<kSlots>(qs, j, K);
+            const float2 *s_prev = pos_buf(pj3);                // positions after step j
             if (staged >= 0 && env_off + staged <= out.cap)
                 write_staged<kN, kNo>(L, s_prev, (uint32_t *)s_nf, staged, env_off, out);
             else
-                emit_rows<kN, kNo, 1>(s, L, s_prev, oo, env_off, out, env_off + my_cnt > out.cap);
+                emit_rows<kN, kNo, 1>(s, L, s_prev, mask, env_off, out, env_off + my_cnt > out.cap);
         }
         wave_sync();
         GSM_ACC(p, L.b, 14, te3);
     };
+    int r3 = 0;                 // k % 3
+    bool relaid_prev = false;   // the previous iteration re-laid the env out (wave-uniform)
     for (int k = 0; k < K; ++k) {
         // lane-derived values re-formed every iteration (an asm barrier): held
         // across the loop they would pin their hoisted addresses in VGPRs
@@ -1392,8 +1405,9 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
 
         // apply_environment_force + integrate_state (as gsm_step_seg_kernel):
         // from s_cur into s_pos
-        const float2 *const s_cur = pos_buf(k);
-        float2 *const s_pos = pos_buf(k + 1);
+        const int r3n = r3 == 2 ? 0 : r3 + 1;   // (k + 1) % 3
+        const float2 *const s_cur = pos_buf(r3);
+        float2 *const s_pos = pos_buf(r3n);
         KernargParams &pc = late_params();
         if (L.agent) {
             const float2 pi = s_cur[m];
@@ -1531,8 +1545,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         }
 
         // publish the workgroup's edge sum of step t
-        const int par = k & 1;
-        if (L.lane == 0) s_bc[par * kWavesPerBlock + wave] = wave_edges;
+        if (L.lane == 0) s_bc[r3 * kWavesPerBlock + wave] = wave_edges;
         GSM_ACC(p, L.b, 10, tw0);   // the step's work
         GSM_TNOW(tw1);
         __syncthreads();
@@ -1540,12 +1553,12 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         if (threadIdx.x == 0) {
             int sum = 0;
             for (int w = 0; w < kWavesPerBlock; ++w) {
-                s_pre[par * kWavesPerBlock + w] = sum;
-                sum += s_bc[par * kWavesPerBlock + w];
+                s_pre[r3 * kWavesPerBlock + w] = sum;
+                sum += s_bc[r3 * kWavesPerBlock + w];
             }
-            __hip_atomic_store((gu64 *)(q.roll.gran + (int64_t)k * gridDim.x + blockIdx.x),
-                               ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)sum, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            const int cs = q.roll.csum_stride;
+            prefix_publish(q.roll.gran + (int64_t)k * gridDim.x, q.roll.csum + (int64_t)k * nc * cs, cs,
+                           (int)blockIdx.x, etag | (uint32_t)(k + 1), (uint32_t)sum);
             // the last step's sums for the emit launch that follows, in the
             // config's workgroup layout: with G envs per wave the last of the
             // G rollout workgroups of a slot adds the others' granules
@@ -1560,8 +1573,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
                         const uint32_t tag = etag | (uint32_t)(k + 1);
                         int tot = sum;
                         for (int j = first; j < r; ++j) {
-                            uint64_t x = __hip_atomic_load((const gu64 *)(gk + j), __ATOMIC_RELAXED,
-                                                           __HIP_MEMORY_SCOPE_AGENT);
+                            uint64_t x = gran_ld(gk + j);
                             if ((uint32_t)(x >> 32) != tag) x = roll_wait(gk + j, tag, q.roll.status);
                             tot += (int)(uint32_t)x;
                         }
@@ -1571,33 +1583,51 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             }
         }
         if (k == K - 1) GSM_RSTAMP(p, L.b, 4);
-        if (k > 0) emit_prev(k, L);
+        // the edges of step t - 2 (row masks kept in s_row, positions after
+        // it in buffer (k + 2) % 3, its counts in s_bc[(k + 1) % 3])
+        if (k >= 2) emit_step(k - 2, r3n == 2 ? 0 : r3n + 1, r3n, s_row[L.lane], pacing() ? k : 0, L);
         // this workgroup's step into its CU's pace counter (read back in the
         // next iteration's emission)
         if (threadIdx.x == 0 && pacing())
             (void)__hip_atomic_fetch_add(pace_ctr(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // keep step t for the next iteration's emission and sweep
+        // keep step t - 1's row masks for the next iteration's emission and
+        // step t's for its sweep
+        s_row[L.lane] = oo;
         oo = row;
         cand_prev = L.agent ? cand : 0ull;
-        if (__builtin_expect(relaid, 0)) {   // wave-uniform: the new episode's statics into the other buffer
-            for (int e = N + m; e < E; e += kWave) pos_buf(k)[e] = s_pos[e];
+        // A re-layout (iteration k) puts the new episode's statics into
+        // buffer (k + 1) % 3; the other two still hold the old ones, which the
+        // emissions of steps t - 2 and t - 1 (this and the next iteration)
+        // read. So they are copied into buffer (k + 2) % 3 now, after this
+        // iteration's emission, and into buffer k % 3 = (k + 3) % 3 at the end
+        // of the next iteration, after its emission: each before the sweep
+        // that reads it.
+        const bool relaid_now = __any(relaid);
+        if (__builtin_expect(relaid_now || relaid_prev, 0)) {
+            float2 *const dst = pos_buf(r3n == 2 ? 0 : r3n + 1);
+            for (int e = N + m; e < E; e += kWave) dst[e] = s_pos[e];
         }
+        relaid_prev = relaid_now;
         if constexpr (!kFused) u = roll_force<kFmt>(late_params(), anext, L.agent);
         arow = nrow;
+        r3 = r3n;
         wave_sync();
     }
-    {   // the tail: the last step's edges
+    {   // the tail: the last two steps' edges (r3 = K % 3)
         Lane L = L0;
         asm volatile("" : "+v"(L.lane), "+v"(L.m));
         GSM_RSTAMP(p, L.b, 5);
-        emit_prev(K, L);
+        const int rm1 = r3 == 0 ? 2 : r3 - 1;   // (K - 1) % 3
+        if (K >= 2) emit_step(K - 2, rm1, rm1 == 0 ? 2 : rm1 - 1, s_row[L.lane], 0, L);
+        GSM_RSTAMP(p, L.b, 6);
+        emit_step(K - 1, r3, rm1, oo, 0, L);
         GSM_RSTAMP(p, L.b, 7);
     }
     // the final state (what the next launch or an eager step reads)
     KernargParams &q = late_params();
     if (wave_live) {
         float2 *const pos_b = q.pos + eb * E;
-        const float2 *const s_pos = pos_buf(K);
+        const float2 *const s_pos = pos_buf(r3);
         if (L0.lane < E) pos_b[L0.lane] = s_pos[L0.lane];
         if (L0.lane + kWave < E) pos_b[L0.lane + kWave] = s_pos[L0.lane + kWave];
         if (L0.agent) {
@@ -2144,7 +2174,7 @@ size_t roll_kernel_lds(const DevParams &p) {
     if (p.N == n && p.No == no) return (size_t)kWavesPerBlock * pack_lds_wave<n, no>() + 4 * kWavesPerBlock;
     GSM_PACK_SHAPES(GSM_PICK)
 #undef GSM_PICK
-    return (size_t)kWavesPerBlock * roll_lds_wave(p.N, p.E) + 4 * (4 * kWavesPerBlock + 4);
+    return (size_t)kWavesPerBlock * roll_lds_wave(p.N, p.E) + 4 * (6 * kWavesPerBlock + 4);
 }
 
 const void *emit_seg_kernel_fn(const DevParams &p) {

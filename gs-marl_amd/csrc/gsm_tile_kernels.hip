@@ -862,9 +862,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             int ex = roll_lookback(q.roll.gran + kb, q.roll.gran + (int64_t)K * gridDim.x + kb, etag | (uint32_t)k,
                                    q.roll.status, lane);
             if (lane == 0) {
-                __hip_atomic_store((gu64 *)(late_params().roll.gran + (int64_t)K * gridDim.x + kb + b),
-                                   ((uint64_t)(etag | (uint32_t)k) << 32) | (uint32_t)(ex + prev_edges),
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                gran_st(late_params().roll.gran + (int64_t)K * gridDim.x + kb + b,
+                        ((uint64_t)(etag | (uint32_t)k) << 32) | (uint32_t)(ex + prev_edges));
                 // (an offset past the capacity is a legal overflow of a small
                 // slot: edge_ptr keeps it, emit_env stops its writes at the
                 // capacity)
@@ -1037,9 +1036,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             KernargParams &q = late_params();
             q.ro.done[(kSlots ? k * q.ro.done_s : 0) + b] = done ? 1 : 0;
             if (kSlots || k == K - 1) q.ro.ecount[(kSlots ? k * q.ro.ec_s : 0) + b] = edges;
-            __hip_atomic_store((gu64 *)(q.roll.gran + (int64_t)k * gridDim.x + b),
-                               ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)edges, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+            gran_st(q.roll.gran + (int64_t)k * gridDim.x + b, ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)edges);
         }
         GSM_ACC(late_params(), wid, 4, tp3);   // node features, publish
         }   // k < K

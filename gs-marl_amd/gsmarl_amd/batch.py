@@ -323,13 +323,13 @@ class GpuBatchEnv:
         self._chk(self.lib.gsm_graph_info(self._h, int(slot), C.byref(steps), C.byref(fused)), "gsm_graph_info")
         return bool(fused.value)
 
-    def roll_gave_up(self) -> bool:
+    def roll_gave_up(self) -> int:
         """Whether a bounded in-launch wait (a fused rollout launch, or the
         ragged lagged chain's staging wait) timed out since the last call
         (outputs of that launch invalid); clears the flag. Synchronises."""
         v = C.c_int32()
         self._chk(self.lib.gsm_graph_roll_status(self._h, C.byref(v)), "gsm_graph_roll_status")
-        return bool(v.value)
+        return v.value   # truthy: the reason code (gsm.h gsm_graph_roll_status)
 
     def roll_placement(self) -> tuple:
         """(dealt, fell_back): ragged mixed rollout launches since the last

@@ -294,21 +294,27 @@ int gsm_graph_capture_into(gsm_handle *h, int32_t slot, const void *actions, int
                            int32_t n_actions, int32_t n_steps, int action_fmt, const gsm_outputs *per_step);
 /* Launch the graph in `slot` on `stream` (stream-ordered, asynchronous). A
  * rollout slot (GSM_GRAPH_ROLL, or a rollout buffer's single launch) is its one
- * kernel launched directly, with a fresh launch epoch for its hand-off tags;
- * the rollout slots of a handle share its state and scratch, so their launches
- * never overlap: a launch on a different stream than the handle's previous
- * rollout launch first waits for that stream (host-side synchronisation). */
+ * kernel launched directly, with a fresh launch epoch for its hand-off tags and
+ * its half of the slot's pacing counters; so it cannot be recorded into a
+ * stream capture (GSM_ESTATE on a capturing stream: capture the per-step chain
+ * instead). The rollout slots of a handle share its state and scratch, so their
+ * launches never overlap: a launch on a different stream than the handle's
+ * previous rollout launch first waits, on the device, for an event the library
+ * records behind every rollout launch (no host synchronisation; the previous
+ * stream may have been destroyed since). */
 int gsm_graph_launch(gsm_handle *h, int32_t slot, void *stream);
 /* The graph in `slot`: its step count (0 if none) and whether it is one
  * fused rollout launch (GSM_GRAPH_ROLL, or gsm_graph_capture_into on a
  * rollout buffer) rather than a per-step chain. */
 int gsm_graph_info(gsm_handle *h, int32_t slot, int32_t *steps, int32_t *fused);
-/* After graph launches have completed: *gave_up = 1 if any bounded in-launch
- * wait (a rollout launch's CSR hand-off, or the ragged lagged chain's staging
- * wait) timed out, or an in-launch check failed (an out-of-range CSR offset,
- * a doubly claimed env, a placement slot outside its table), since the last
- * call (that launch's outputs are then invalid), else 0. Clears the flag.
- * Synchronises (reads a device word). */
+/* After graph launches have completed: *gave_up = a non-zero reason code if
+ * any bounded in-launch wait timed out (1: a rollout launch's CSR hand-off, or
+ * the ragged lagged chain's staging wait) or an in-launch check failed (2: an
+ * out-of-range CSR offset, 4: a doubly claimed env, 5: a placement slot
+ * outside its table; 6, in a checked build (-DGSM_CHECKED): a hand-off granule
+ * or slab address outside its allocation) since the last call (that launch's
+ * outputs are then invalid), else 0. Clears the flag. Synchronises (reads a
+ * device word). */
 int gsm_graph_roll_status(gsm_handle *h, int32_t *gave_up);
 /* Ragged mixed rollouts deal their envs to the SIMDs by estimated cost when
  * every wave of the launch is resident (else env = wave index; same outputs

@@ -65,6 +65,24 @@ def main():
 
     res = {"K": a.K, "N": a.N, "B": a.B, "lib": os.environ.get("GSM_LIB_PATH", "libgsm.so")}
     res["sync_only_us"] = med(wall(lambda: None, a.R))
+    # the host side of one replay call alone (returns before the kernel runs):
+    # GpuBatchEnv.replay (Python, ctypes, current-stream lookup) and the bare
+    # C call with the stream pointer cached
+    import ctypes as C
+    calls, bare = [], []
+    sp = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    for _ in range(a.R):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        env.replay(0)
+        calls.append((time.perf_counter() - t0) * 1e6)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        env.lib.gsm_graph_launch(env._h, 0, sp)
+        bare.append((time.perf_counter() - t0) * 1e6)
+    torch.cuda.synchronize(dev)
+    res["replay_call_us"] = med(calls)
+    res["bare_launch_call_us"] = med(bare)
     res["tiny_op_us"] = med(wall(lambda: x.add_(1), a.R))
     res["roll1_us"] = med(wall(lambda: env.replay(1), a.R))
     res[f"roll{a.K}_us"] = med(wall(lambda: env.replay(0), a.R))

@@ -2,10 +2,11 @@
 envs; diagnostic -DGSM_STAMPS build, run with GSM_LIB_PATH pointing at it):
 per wave, s_memrealtime (100 MHz) at the marks of gsm_roll_seg_kernel —
 0 entry, 1 state loaded, 2 step 0 physics, 3 step 0 sweep, 4 step K-1
-published, 5 tail start, 6 tail offset known (look-back), 7 tail emitted,
-8 final state stored; and s_memtime cycles summed per phase over the steps
-(slots 10-14: the step's work, the publish barrier, the look-back of wave 0,
-the wait for it, staging + emission). Prints, per mark, the percentiles over waves of the time
+published, 5 tail start, 6 step K-2 emitted, 7 step K-1 emitted, 8 final
+state stored; 9 HW_ID | XCC_ID << 32 (where the wave ran); and s_memtime
+cycles summed per phase over the steps (slots 10-14: the step's work, the
+publish barrier, the CSR prefix of wave 0, the wait for it, staging +
+emission). Prints, per mark, the percentiles over waves of the time
 since the first wave's entry, for an eager env.step (a K = 1 launch) and for a
 K-step graph replay (K = ROLL_K, default 20).
 
@@ -30,7 +31,7 @@ st = torch.zeros(B, 16, dtype=torch.int64, device=dev)
 env.lib.gsm_debug_set_stamps(env._h, C.c_void_p(st.data_ptr()))
 acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=dev)
 env.reset(seed=5, sync_edges=False)
-MARKS = ["entry", "loaded", "physics0", "sweep0", "published_last", "tail", "tail_offset", "tail_emitted", "stored"]
+MARKS = ["entry", "loaded", "physics0", "sweep0", "published_last", "tail", "tail_emit1", "tail_emit2", "stored"]
 
 
 def timeline():
@@ -65,7 +66,7 @@ e1.record()
 torch.cuda.synchronize()
 qq = st.cpu().numpy().astype(np.int64)
 w0 = np.arange(B) % 4 == 0
-PH = ["work", "publish_barrier", "lookback", "lookback_wait", "stage_emit"]
+PH = ["work", "publish_barrier", "prefix", "prefix_wait", "stage_emit"]
 res[f"replay_K{K}"] = {"events_us": e0.elapsed_time(e1) * 1e3, "marks_us": timeline(),
                        "wave0_cycles_per_step": {n: float(qq[w0, 10 + i].mean() / K) for i, n in enumerate(PH)},
                        "other_waves_cycles_per_step": {n: float(qq[~w0, 10 + i].mean() / K) for i, n in enumerate(PH)}}
