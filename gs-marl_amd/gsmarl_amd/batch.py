@@ -62,7 +62,9 @@ class GpuBatchEnv:
     def __init__(self, cfg: EnvConfig, device="cuda"):
         self.cfg = cfg
         self.device = _require_gpu(device)
+        self._dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
         self.lib = _lib.load()
+        self._launch = self.lib.gsm_graph_launch
         self.sizes = _lib.query_sizes(cfg, self.lib)
         self._ccfg = _lib.make_config(cfg)
         h = C.c_void_p()
@@ -113,7 +115,9 @@ class GpuBatchEnv:
 
     # ------------------------------------------------------------------ utils
     def _stream(self):
-        return C.c_void_p(torch.cuda.current_stream(self.device).cuda_stream)
+        # the raw handle of the current stream (torch's own accessor: no
+        # Stream object built per call)
+        return C.c_void_p(torch._C._cuda_getCurrentRawStream(self._dev_index))
 
     def _chk(self, rc, what):
         _lib.check(self.lib, rc, self._h, what)
@@ -314,7 +318,11 @@ class GpuBatchEnv:
 
     @_ranged("gsm.replay")
     def replay(self, slot: int = 0) -> None:
-        self._chk(self.lib.gsm_graph_launch(self._h, int(slot), self._stream()), "gsm_graph_launch")
+        # (the hot path of a training loop: one C call, the error path only
+        # on a non-zero return)
+        rc = self._launch(self._h, slot, torch._C._cuda_getCurrentRawStream(self._dev_index))
+        if rc:
+            self._chk(rc, "gsm_graph_launch")
 
     def graph_is_rollout(self, slot: int = 0) -> bool:
         """Whether graph ``slot`` is one fused rollout launch (GSM_GRAPH_ROLL,

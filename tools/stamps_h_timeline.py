@@ -58,6 +58,13 @@ res["eager_step"] = {"events_us": e0.elapsed_time(e1) * 1e3, "marks_us": timelin
 env.capture(acts, K, slot=0, kernels="roll")
 for _ in range(3):
     env.replay(0)
+# ROLL_START=s: the timed replay starts at step s of the episode (e.g. 90: it
+# holds the episode boundary, every env auto-resetting in the same step)
+start = int(os.environ.get("ROLL_START", 0))
+env.reset(seed=5, sync_edges=False)
+if start:
+    env.capture(acts, start, slot=1, kernels="roll")
+    env.replay(1)
 torch.cuda.synchronize()
 st.zero_()
 e0.record()
@@ -67,7 +74,7 @@ torch.cuda.synchronize()
 qq = st.cpu().numpy().astype(np.int64)
 w0 = np.arange(B) % 4 == 0
 PH = ["work", "publish_barrier", "prefix", "prefix_wait", "stage_emit"]
-res[f"replay_K{K}"] = {"events_us": e0.elapsed_time(e1) * 1e3, "marks_us": timeline(),
+res[f"replay_K{K}_from{start}"] = {"events_us": e0.elapsed_time(e1) * 1e3, "marks_us": timeline(),
                        "wave0_cycles_per_step": {n: float(qq[w0, 10 + i].mean() / K) for i, n in enumerate(PH)},
                        "other_waves_cycles_per_step": {n: float(qq[~w0, 10 + i].mean() / K) for i, n in enumerate(PH)}}
 hw = qq[:, 9]
@@ -84,11 +91,11 @@ if hw.any():
         wgs = np.unique(wg[sel])
         for r, g in enumerate(wgs):
             by_rank.setdefault(r, []).append(float(fin[sel][wg[sel] == g].max()))
-    res[f"replay_K{K}"]["finish_us_by_rank_on_cu"] = {
+    res[f"replay_K{K}_from{start}"]["finish_us_by_rank_on_cu"] = {
         int(r): {"n": len(v), "mean": round(float(np.mean(v)), 2), "min": round(float(np.min(v)), 2),
                  "max": round(float(np.max(v)), 2)} for r, v in sorted(by_rank.items())}
-    res[f"replay_K{K}"]["cus"] = int(len(np.unique(cu)))
-    res[f"replay_K{K}"]["simds"] = int(len(np.unique(simd)))
+    res[f"replay_K{K}_from{start}"]["cus"] = int(len(np.unique(cu)))
+    res[f"replay_K{K}_from{start}"]["simds"] = int(len(np.unique(simd)))
     out = os.environ.get("STAMPS_NPZ")
     if out:
         np.savez_compressed(out, stamps=qq, hw=hw)
