@@ -1484,6 +1484,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             reset = true;
             if (m == 0) late_params().ep_last[L.b] = acc;
         }
+        GSM_TNOW(tr0);
         if (__any(reset)) {
             // auto-reset: scenario.reset_world, then the graph part again
             if (reset) {
@@ -1510,6 +1511,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
                 Fn = Fn2;
             }
         }
+        GSM_ACC(p, L.b, 15, tr0);   // diagnostic builds: the re-layout (and the test for it)
         const bool relaid = reset;
         if (!L.live) row = 0;
         if constexpr (kFused) {

@@ -76,7 +76,9 @@ w0 = np.arange(B) % 4 == 0
 PH = ["work", "publish_barrier", "prefix", "prefix_wait", "stage_emit"]
 res[f"replay_K{K}_from{start}"] = {"events_us": e0.elapsed_time(e1) * 1e3, "marks_us": timeline(),
                        "wave0_cycles_per_step": {n: float(qq[w0, 10 + i].mean() / K) for i, n in enumerate(PH)},
-                       "other_waves_cycles_per_step": {n: float(qq[~w0, 10 + i].mean() / K) for i, n in enumerate(PH)}}
+                       "other_waves_cycles_per_step": {n: float(qq[~w0, 10 + i].mean() / K) for i, n in enumerate(PH)},
+                       # slot 15: cycles in the re-layout block (auto-reset), summed over the launch
+                       "relayout_cycles_per_launch": float(qq[:, 15].mean())}
 hw = qq[:, 9]
 if hw.any():
     # where each wave ran (slot 9: HW_ID | XCC_ID << 32) against when it
