@@ -426,6 +426,47 @@ __device__ __forceinline__ void xfer_grp_publish(const Xfer &x, uint64_t l, int 
     if (lane == 0) xfer_st(x.grp + (int64_t)s * x.NG + (w >> 6), tag, (uint32_t)sum);
 }
 
+// ---- pacing of the rollouts (round 5; gsm_roll_seg_kernel, gsm_roll_tile_kernel)
+// A SIMD issues its ready waves oldest first below the user priority
+// (s_setprio), and a CU holds several workgroups of a rollout (eight at H),
+// dispatched one residency rank at a time (blockIdx / 256 at H). Measured per
+// CU, the rank-0 workgroup finished a 20-step launch at 109 us and rank 7 at
+// 210 us, in exact rank order on every CU, and the same without any hand-off
+// (profiles/r5_pace): the last ranks' final steps run on a CU already half
+// empty. Some order between ranks helps the look-back — a workgroup finds
+// the inclusive prefixes of the rank before it already published — but not
+// twelve steps of it. So each workgroup counts its finished steps into its
+// CU's counter (one atomic add per step, the counter loaded back beside the
+// next step's look-back loads; its rank = the arrivals before its own, read
+// at entry) and sets its waves' priority from its own
+// steps against a target: the CU's mean plus (c - rank) x q / 4 steps,
+// c = (arrivals - 1) / 2 — ahead of the target by half a step or more 0,
+// behind by as much 2, else 1. Priority only orders issue: outputs are
+// unchanged. A counter is one 32-bit word: arrivals in the top 8 bits, steps
+// in the low 24 (8 workgroups x 4094 steps < 2^24).
+constexpr uint32_t kPaceArrive = 1u << 24;
+__device__ __forceinline__ uint32_t pace_key() {
+    const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);          // HW_ID
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;   // XCC_ID
+    return (xcc << 8 | ((hw >> 13) & 7u) << 5 | ((hw >> 12) & 1u) << 4 | ((hw >> 8) & 15u)) * kPaceStride;
+}
+// the level from the CU counter as loaded after this workgroup's `done`-th
+// step was added to it
+__device__ __forceinline__ int pace_level(uint32_t fv, int done, int rank, int q) {
+    const int arr = (int)(fv >> 24), tot = (int)(fv & (kPaceArrive - 1));
+    // 8 x arrivals x (own steps - the CU's mean - (c - rank) x q / 4)
+    const int x = 8 * (done * arr - tot) - arr * (arr - 1 - 2 * rank) * q;
+    return x >= 4 * arr ? 0 : x <= -4 * arr ? 2 : 1;
+}
+__device__ __forceinline__ void pace_set(int lvl) {   // lvl wave-uniform
+    if (lvl == 0)
+        __builtin_amdgcn_s_setprio(0);
+    else if (lvl == 1)
+        __builtin_amdgcn_s_setprio(1);
+    else
+        __builtin_amdgcn_s_setprio(2);
+}
+
 // ---- one-hop CSR prefix of the one-env-per-wave segmented rollout (round 5)
 // The packed offset of workgroup w's edges of step s is the sum of the edge
 // counts of every workgroup before it. Two kinds of words per step:

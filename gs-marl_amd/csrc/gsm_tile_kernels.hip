@@ -826,6 +826,20 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     int ep = p.episode[b];
     float2 acc = p.ep_acc[b];
     if (tid == 0) s_deg[0] = s_deg[1] = 0;
+    // pacing (gsm_device.h pace_level): this workgroup's CU counter (its
+    // arrival now, a step after each step, its rank = the arrivals before it;
+    // the address re-formed at each use), the slot's next counters zeroed
+    auto pacing = [] { return late_params().roll.pace != nullptr; };
+    auto pace_ctr = [] { return (gu32 *)(late_params().roll.pace + pace_key()); };
+    if (pacing()) {
+        KernargParams &qz = late_params();
+        for (int i = b * kTileBlock + tid; i < kPaceKeys; i += gridDim.x * kTileBlock)
+            __hip_atomic_store((gu32 *)(qz.roll.pace_next + i * kPaceStride), 0u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        if (tid == 0)
+            s_x[3] = (int)(__hip_atomic_fetch_add(pace_ctr(), kPaceArrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >>
+                           24);
+    }
     const int K = p.roll.K, n_act = p.roll.n_actions;
     const uint32_t etag = roll_epoch_tag(p.roll.epoch);     // this launch's tag base
     int arow = p.roll.t_first % n_act;
@@ -859,9 +873,14 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             GSM_TNOW(tp4);
             const int64_t kb = (int64_t)(k - 1) * gridDim.x;
             KernargParams &q = late_params();
+            // (the CU's pace counter loaded beside the look-back's granules)
+            const uint32_t pv = k < K && pacing() ? __hip_atomic_load(pace_ctr(), __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                                  : 0u;
             int ex = roll_lookback(q.roll.gran + kb, q.roll.gran + (int64_t)K * gridDim.x + kb, etag | (uint32_t)k,
                                    q.roll.status, lane);
             if (lane == 0) {
+                s_x[1] = (int)pv;
                 gran_st(late_params().roll.gran + (int64_t)K * gridDim.x + kb + b,
                         ((uint64_t)(etag | (uint32_t)k) << 32) | (uint32_t)(ex + prev_edges));
                 // (an offset past the capacity is a legal overflow of a small
@@ -934,6 +953,11 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             s_np[i] = make_float2(pi.x + v.x * late_params().dt, pi.y + v.y * late_params().dt);
         }
         __syncthreads();
+        // this workgroup's pace level (from the counter the last wave loaded
+        // at the top of the iteration, published by the barrier above)
+        if (k > 0 && pacing())
+            pace_set(pace_level((uint32_t)__builtin_amdgcn_readfirstlane(s_x[1]), k,
+                                __builtin_amdgcn_readfirstlane(s_x[3]), late_params().roll.pace_q));
         for (int i = tid; i < N; i += kTileBlock) s_pos[i] = s_np[i];
         __syncthreads();
         t += 1;
@@ -1037,6 +1061,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             q.ro.done[(kSlots ? k * q.ro.done_s : 0) + b] = done ? 1 : 0;
             if (kSlots || k == K - 1) q.ro.ecount[(kSlots ? k * q.ro.ec_s : 0) + b] = edges;
             gran_st(q.roll.gran + (int64_t)k * gridDim.x + b, ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)edges);
+            if (pacing()) (void)__hip_atomic_fetch_add(pace_ctr(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         GSM_ACC(late_params(), wid, 4, tp3);   // node features, publish
         }   // k < K
