@@ -938,23 +938,22 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     drop_slot(sl);
     // a 16-byte header (unused), then 8-byte granules. Ragged and packed
     // small envs: per-wave counts [K][xW] and group sums [K][xNG]; the tile
-    // path: aggregates [K][nb] and inclusive prefixes [K][nb] (look-back), then
-    // two halves of pace counters (gsm_device.h pace_level); the other
-    // segmented shapes (one env per wave): aggregates [K][nb], two halves of
-    // chunk sums [K][nc] kCsumStride apart (gsm_device.h roll_prefix) and two
-    // halves of pace counters. Zeroed once here — granules are tagged with the launch
+    // path and the other segmented shapes (one env per workgroup or per
+    // wave): aggregates [K][nb], two halves of chunk sums [K][nc] kCsumStride
+    // apart (gsm_device.h roll_prefix) and two halves of pace counters
+    // (gsm_device.h pace_level). Zeroed once here — granules are tagged with the launch
     // epoch, so replays never clear them; the untagged chunk sums and counters
     // are zeroed by the launch before the one that uses them
     // (ragged: then the placement words, gsm::PlaceArea)
-    const bool paced = !per_wave, one_hop = paced && !tile;
+    const bool one_hop = !per_wave;   // one-hop prefix and pacing: the one-env-per-wave and tile rollouts
     const size_t nc = ((size_t)nb + gsm::kPrefixChunk - 1) / gsm::kPrefixChunk;
     if (one_hop && nc > (size_t)gsm::kWave) {   // roll_prefix: one chunk sum per lane
         if (fallback) return kRollIneligible;
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: more than 4096 workgroups in one rollout launch");
     }
     const size_t csum_half = one_hop ? (size_t)K * nc * kCsumStride : 0;   // u64
-    const size_t pace_words = paced ? (size_t)gsm::kPaceKeys * gsm::kPaceStride : 0;   // u32, per half
-    const size_t gran_alloc = 16 + ((size_t)K * (per_wave ? (size_t)(xW + xNG) : one_hop ? (size_t)nb : 2 * (size_t)nb) +
+    const size_t pace_words = one_hop ? (size_t)gsm::kPaceKeys * gsm::kPaceStride : 0;   // u32, per half
+    const size_t gran_alloc = 16 + ((size_t)K * (per_wave ? (size_t)(xW + xNG) : (size_t)nb) +
                                     2 * csum_half) * sizeof(uint64_t) +
                               2 * pace_words * sizeof(uint32_t) +
                               (ragged ? gsm::PlaceArea::words(xW) * sizeof(uint64_t) : 0);
@@ -982,9 +981,9 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         else
             pace_q = std::max(0, atoi(ev));
     }
-    if (paced) {   // (the tile path: pace counters after its look-back granules)
-        uint64_t *const after = sl.gran + 2 + (size_t)K * (one_hop ? 1 : 2) * nb;
-        sl.csum = one_hop ? after : nullptr;
+    if (one_hop) {
+        uint64_t *const after = sl.gran + 2 + (size_t)K * nb;
+        sl.csum = after;
         sl.csum_half = (int64_t)csum_half;
         sl.pace = pace_on ? (uint32_t *)(after + 2 * csum_half) : nullptr;
     }

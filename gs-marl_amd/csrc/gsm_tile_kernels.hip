@@ -775,11 +775,11 @@ __global__ __launch_bounds__(kTileBlock) void gsm_emit_tile_kernel(DevParams p) 
 // outputs (node features, reward, cost, done) are written every step, the
 // state once after the loop. Same operations as gsm_step_tile_kernel in the
 // same order: bit-identical outputs.
-constexpr int kRollTileScr = 2048;   // staged edge words (C3: ~390 edges per env; else direct writes)
+constexpr int kRollTileScr = 1536;   // staged edge words (C3: ~390 edges per env; else direct writes)
 
 size_t roll_tile_kernel_lds(const DevParams &p) {
-    return (size_t)p.wave_lds_step + 8 * (size_t)p.E + 16 + 8 * kTileWaves + 4 * kRollTileScr +
-           8 * (size_t)p.W * (2 * p.M + p.N);
+    return (size_t)p.wave_lds_step + 16 * (size_t)p.E + 16 + 8 * kTileWaves + 4 * kRollTileScr +
+           8 * (size_t)p.W * (3 * p.M + p.N);
 }
 
 // kN > 0: compiled for kN agents and kNo obstacles (C3: 96 + 96), so the
@@ -809,15 +809,17 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         q += 8 * No * W;
         sym.flag = (int *)q;
     }
-    float2 *s_prev = (float2 *)(smem + p.wave_lds_step);   // [E] positions of the previous step
-    int *s_x = (int *)(s_prev + E);                        // [4]
+    // [2][E] positions after step k - 2 (and k), by parity: iteration k emits
+    // the edges of step k - 2
+    float2 *s_prv = (float2 *)(smem + p.wave_lds_step);
+    int *s_x = (int *)(s_prv + 2 * E);                     // [4]
     int *s_red = s_x + 4;                                  // [2 * kTileWaves] emit_env exchange
     uint32_t *s_scr = (uint32_t *)(s_red + 2 * kTileWaves);
-    uint64_t *s_rm = (uint64_t *)(s_scr + kRollTileScr);   // [2][M][W] row masks, step k at k & 1
-    uint64_t *s_cm = s_rm + 2 * M * W;                     // [N][W] contact words
+    uint64_t *s_rm = (uint64_t *)(s_scr + kRollTileScr);   // [3][M][W] row masks, step k at k % 3
+    uint64_t *s_cm = s_rm + 3 * M * W;                     // [N][W] contact words
     const int64_t eb = b;
     const int32_t g0 = (int32_t)(eb * E);
-    for (int w = tid; w < M * W; w += kTileBlock) s_rm[M * W + w] = p.row_mask[eb * M * W + w];
+    for (int w = tid; w < M * W; w += kTileBlock) s_rm[2 * M * W + w] = p.row_mask[eb * M * W + w];
     for (int w = tid; w < N * W; w += kTileBlock) s_cm[w] = p.contact_mask[eb * N * W + w];
 
     for (int e = tid; e < E; e += kTileBlock) s_pos[e] = p.pos[eb * E + e];
@@ -831,6 +833,16 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     // the address re-formed at each use), the slot's next counters zeroed
     auto pacing = [] { return late_params().roll.pace != nullptr; };
     auto pace_ctr = [] { return (gu32 *)(late_params().roll.pace + pace_key()); };
+    // the one-hop CSR prefix (gsm_device.h roll_prefix): chunks of 64
+    // workgroups; the slot's next launch's chunk sums zeroed
+    const int nc = ((int)gridDim.x + kPrefixChunk - 1) / kPrefixChunk;
+    {
+        KernargParams &qz = late_params();
+        const int cs = qz.roll.csum_stride, n = qz.roll.K * nc;
+        for (int i = b * kTileBlock + tid; i < n; i += gridDim.x * kTileBlock)
+            __hip_atomic_store((gu64 *)(qz.roll.csum_next + (int64_t)i * cs), 0ull, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
     if (pacing()) {
         KernargParams &qz = late_params();
         for (int i = b * kTileBlock + tid; i < kPaceKeys; i += gridDim.x * kTileBlock)
@@ -843,17 +855,18 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     const int K = p.roll.K, n_act = p.roll.n_actions;
     const uint32_t etag = roll_epoch_tag(p.roll.epoch);     // this launch's tag base
     int arow = p.roll.t_first % n_act;
-    int prev_edges = 0, bad = 0;
+    int edges_m1 = 0, edges_m2 = 0, last_edges = 0, bad = 0;   // edge counts of steps k - 1, k - 2, K - 1
+    int r3 = 0;                                               // k % 3
     __syncthreads();
 
-    // iterations 0..K-1 run step k and emit step k-1; iteration K (the tail)
-    // only emits step K-1
+    // iterations 0..K-1 run step k and emit step k-2; iterations K and K+1
+    // (the tail) only emit steps K-2 and K-1
     // Inside the loop the launch's flags and constants are read through the
     // kernarg view at their use (late_params()): read from `p` the compiler
     // hoists them out of the loop and holds them in SGPRs, spilled to VGPR
     // lanes at 8 waves per SIMD (gsm_roll_seg_kernel).
     GSM_RSTAMP(p, b * kTileWaves + (tid >> 6), 8);
-    for (int k = 0; k <= K; ++k) {
+    for (int k = 0; k <= K + 1; ++k) {
         // thread-derived values re-formed every iteration (an asm barrier): held
         // across the loop their hoisted addresses would pin VGPRs
         int tid = (int)threadIdx.x;
@@ -862,27 +875,31 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         const int wid = b * kTileWaves + wave;   // (diagnostic stamps)
         (void)wid;
         GSM_TNOW(tp0);
-        uint64_t *const rout = s_rm + (k & 1) * M * W;
-        const uint64_t *const rkeep = s_rm + ((k + 1) & 1) * M * W;   // the previous step's masks
+        const int r3n = r3 == 2 ? 0 : r3 + 1, r3p = r3 == 0 ? 2 : r3 - 1;   // (k + 1) % 3, (k - 1) % 3
+        uint64_t *const rout = s_rm + r3 * M * W;
+        const uint64_t *const rkeep = s_rm + r3p * M * W;   // the previous step's masks
+        const uint64_t *const remit = s_rm + r3n * M * W;   // step k - 2's masks (emitted this iteration)
         int edges = 0;
-        // the previous step's CSR offset: the look-back by the last wave, idle
-        // in the physics below (agents 0..N-1 on the first threads), so its
-        // latency overlaps the step; read by the emission after the step
-        // (s_x[2], published by the step's barriers)
+        // step k - 2's CSR offset: the one-hop prefix (published an iteration
+        // ago by every workgroup in step: one load per lane) by the last wave,
+        // idle in the physics below (agents 0..N-1 on the first threads), so
+        // its latency overlaps the step; read by the emission after the step
+        // (s_x[2], published by the step's barriers); the CU's pace counter
+        // loaded beside it
         if (k > 0 && wave == kTileWaves - 1) {
             GSM_TNOW(tp4);
-            const int64_t kb = (int64_t)(k - 1) * gridDim.x;
             KernargParams &q = late_params();
-            // (the CU's pace counter loaded beside the look-back's granules)
             const uint32_t pv = k < K && pacing() ? __hip_atomic_load(pace_ctr(), __ATOMIC_RELAXED,
                                                                        __HIP_MEMORY_SCOPE_AGENT)
                                                   : 0u;
-            int ex = roll_lookback(q.roll.gran + kb, q.roll.gran + (int64_t)K * gridDim.x + kb, etag | (uint32_t)k,
-                                   q.roll.status, lane);
+            int ex = 0;
+            if (k >= 2) {
+                const int cs = q.roll.csum_stride;
+                ex = roll_prefix(q.roll.gran + (int64_t)(k - 2) * gridDim.x, q.roll.csum + (int64_t)(k - 2) * nc * cs,
+                                 cs, etag | (uint32_t)(k - 1), q.roll.status, lane);
+            }
             if (lane == 0) {
                 s_x[1] = (int)pv;
-                gran_st(late_params().roll.gran + (int64_t)K * gridDim.x + kb + b,
-                        ((uint64_t)(etag | (uint32_t)k) << 32) | (uint32_t)(ex + prev_edges));
                 // (an offset past the capacity is a legal overflow of a small
                 // slot: edge_ptr keeps it, emit_env stops its writes at the
                 // capacity)
@@ -893,9 +910,9 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                 }
                 s_x[2] = ex;
             }
-            GSM_ACC(late_params(), wid, 5, tp4);   // look-back (last wave)
+            GSM_ACC(late_params(), wid, 5, tp4);   // the prefix (last wave)
         }
-        if (k == K) __syncthreads();   // (the tail: no step; s_x[2] for the emission)
+        if (k >= K) __syncthreads();   // (the tail: no step; s_x[2] for the emission)
         if (k < K) {
         bool relaid = false;
         auto relayout = [&]() {   // scenario.reset_world with the Philox layout
@@ -1060,46 +1077,54 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             KernargParams &q = late_params();
             q.ro.done[(kSlots ? k * q.ro.done_s : 0) + b] = done ? 1 : 0;
             if (kSlots || k == K - 1) q.ro.ecount[(kSlots ? k * q.ro.ec_s : 0) + b] = edges;
-            gran_st(q.roll.gran + (int64_t)k * gridDim.x + b, ((uint64_t)(etag | (uint32_t)(k + 1)) << 32) | (uint32_t)edges);
+            const int cs = q.roll.csum_stride;
+            prefix_publish(q.roll.gran + (int64_t)k * gridDim.x, q.roll.csum + (int64_t)k * nc * cs, cs, b,
+                           etag | (uint32_t)(k + 1), (uint32_t)edges);
             if (pacing()) (void)__hip_atomic_fetch_add(pace_ctr(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         GSM_ACC(late_params(), wid, 4, tp3);   // node features, publish
         }   // k < K
-        // the previous step's edges at the offset of the look-back
-        if (k > 0) {
+        // step k - 2's edges at the offset of the prefix (its positions in
+        // s_prv by parity, its masks in buffer (k - 2) % 3)
+        float2 *const s_pk = s_prv + (k & 1) * E;
+        if (k >= 2) {
             GSM_TNOW(tp5);
             int64_t off;
-            emit_env<kN, kNo>(p, roll_edge_sink<kSlots>(late_params(), k - 1, K), s_prev, rkeep,
+            emit_env<kN, kNo>(p, roll_edge_sink<kSlots>(late_params(), k - 2, K), s_pk, remit,
                               tid == 0 ? s_x[2] : 0, &off, s_red, s_scr, kRollTileScr, g0);
             GSM_ACC(late_params(), wid, 6, tp5);   // emission
             if (tid == 0) {
                 KernargParams &q = late_params();
-                int64_t *const eptr = q.ro.eptr + (kSlots ? (k - 1) * q.ro.ep_s : 0);
+                int64_t *const eptr = q.ro.eptr + (kSlots ? (k - 2) * q.ro.ep_s : 0);
                 eptr[b] = off;
-                if (b == late_params().B - 1) eptr[late_params().B] = off + prev_edges;
+                if (b == late_params().B - 1) eptr[late_params().B] = off + edges_m2;
             }
         }
         if (k < K) {
             GSM_TNOW(tp6);
-            __syncthreads();   // s_prev and the staged words read
-            for (int e = tid; e < E; e += kTileBlock) s_prev[e] = s_pos[e];
-            prev_edges = edges;
+            __syncthreads();   // s_pk and the staged words read
+            for (int e = tid; e < E; e += kTileBlock) s_pk[e] = s_pos[e];   // positions after step k
             arow = arow + 1 == n_act ? 0 : arow + 1;
+            if (k == K - 1) last_edges = edges;
             __syncthreads();
             GSM_ACC(late_params(), wid, 7, tp6);   // hand-over to the next step
         }
+        edges_m2 = edges_m1;
+        edges_m1 = edges;
+        r3 = r3n;
     }
     GSM_RSTAMP(p, b * kTileWaves + (tid >> 6), 9);
     // the final state (what the next launch or an eager step reads)
     for (int e = tid; e < E; e += kTileBlock) p.pos[eb * E + e] = s_pos[e];
-    for (int w = tid; w < M * W; w += kTileBlock) p.row_mask[eb * M * W + w] = s_rm[((K - 1) & 1) * M * W + w];
+    const int rl = (K - 1) % 3;   // the last step's masks
+    for (int w = tid; w < M * W; w += kTileBlock) p.row_mask[eb * M * W + w] = s_rm[rl * M * W + w];
     for (int w = tid; w < N * W; w += kTileBlock) p.contact_mask[eb * N * W + w] = s_cm[w];
     for (int i = tid; i < N; i += kTileBlock) p.vel[eb * N + i] = s_vel[i];
     if (tid == 0) {
         p.step_count[b] = t;
         p.episode[b] = ep;
         p.ep_acc[b] = acc;
-        p.block_edge_sum[b] = prev_edges;
+        p.block_edge_sum[b] = last_edges;
         if (p.degenerate) p.degenerate[b] = (uint8_t)((*sym.flag ? kDegCoincident : 0) | (bad ? kDegNonfinite : 0));
     }
 }
