@@ -59,6 +59,7 @@ def _same(ref, env, what):
                                           (24, 8192, 26, 25, "index"),
                                           # C2's shape (the step kernels pack 4 envs per wave, the rollout one)
                                           (3, 64, 12, 5, "index"), (3, 4096, 15, 6, "index"), (3, 4100, 7, 3, "onehot"),
+                                          (3, 333, 9, 4, "cont"),
                                           # the reference's zero-shot navigation sizes (readme.md:75)
                                           (6, 1024, 10, 4, "index"), (6, 37, 7, 3, "cont"), (12, 2048, 9, 5, "onehot"),
                                           (12, 100, 6, 4, "index"),
@@ -316,6 +317,42 @@ def test_eager_one_launch_equals_two_kernels(N, B, monkeypatch):
     for e in envs:
         assert not e.roll_gave_up()
         e.close()
+
+
+@pytest.mark.parametrize("N,B", [(24, 512), (96, 16), (12, 100)])
+def test_eager_one_launch_redirected_outputs(N, B, monkeypatch):
+    """The one-launch eager step (GSM_EAGER_ONE_LAUNCH=1) writing every output
+    into a fresh redirected set per step (gsm_step_into: node features,
+    reward, cost, done, counts, CSR pointers and edges) gives exactly the
+    two-kernel pair's outputs of every step, auto-resets included."""
+    T, EL = 6, 4
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    keys = ("node_feat", "reward", "cost", "done", "edge_count", "edge_ptr")
+    got = []
+    for two in (True, False):
+        if two:
+            monkeypatch.delenv("GSM_EAGER_ONE_LAUNCH", raising=False)
+        else:
+            monkeypatch.setenv("GSM_EAGER_ONE_LAUNCH", "1")
+        env, _ = _env(n_agents=N, n_envs=B, episode_length=EL, seed=13)
+        env.reset(seed=13)
+        steps = []
+        for t in range(T):
+            out = {k: torch.full_like(env.t[k], -7) for k in keys}
+            out["edge_index"] = torch.full_like(env.t["edge_index"], -7)
+            out["edge_attr"] = torch.full_like(env.t["edge_attr"], -7.0)
+            env.step(acts[t], out=out)
+            steps.append(out)
+        torch.cuda.synchronize()
+        assert not env.roll_gave_up()
+        got.append(steps)
+        env.close()
+    for t, (a, b) in enumerate(zip(*got)):
+        for k in keys:
+            assert torch.equal(a[k], b[k]), (t, k)
+        n = int(a["edge_ptr"][-1])
+        assert torch.equal(a["edge_index"][:, :n], b["edge_index"][:, :n]), t
+        assert torch.equal(a["edge_attr"][:n], b["edge_attr"][:n]), t
 
 
 def test_roll_replay_refused_inside_stream_capture():
