@@ -1,7 +1,8 @@
 # Build a diagnostic variant of libgsm.so next to the product library (never
-# loaded unless GSM_LIB_PATH points at it). The only diagnostic flag the
-# sources know is -DGSM_STAMPS (per-wave s_memtime phase stamps, read by
-# tools/stamps*.py). Usage: bash tools/build_variant.sh "NAME:-DFLAG ..." ...
+# loaded unless GSM_LIB_PATH points at it). The sources know two flags:
+# -DGSM_STAMPS (per-wave s_memtime phase stamps, read by tools/stamps*.py) and
+# -DGSM_CHECKED (every rollout hand-off granule and slab address tested against
+# its allocation; status 6 instead of an out-of-range access). Usage: bash tools/build_variant.sh "NAME:-DFLAG ..." ...
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gs-marl_amd/gsmarl_amd/lib/ablate

@@ -39,7 +39,15 @@ def main():
     ap.add_argument("--R", type=int, default=15)
     ap.add_argument("--N", type=int, default=24)
     ap.add_argument("--B", type=int, default=8192)
+    # host wait mode of synchronize: HIP's hipSetDeviceFlags schedule flag,
+    # set before (early) or after (late) the first GPU use
+    ap.add_argument("--sched", choices=["default", "spin", "yield", "block"], default="default")
+    ap.add_argument("--sched-when", choices=["early", "late"], default="early")
     a = ap.parse_args()
+    flag = {"spin": 1, "yield": 2, "block": 4}.get(a.sched)
+    if flag and a.sched_when == "early":
+        import ctypes
+        print("hipSetDeviceFlags", ctypes.CDLL("libamdhip64.so.7").hipSetDeviceFlags(flag), file=sys.stderr)
     dev = torch.device("cuda", 0)
     env = GpuBatchEnv(EnvConfig(n_agents=a.N, n_envs=a.B, seed=1234), dev)
     acts = torch.randint(0, 5, (100, a.B, a.N), dtype=torch.int32, device=dev)
@@ -47,6 +55,9 @@ def main():
     env.capture(acts, 1, slot=1, kernels="roll")
     env.capture(acts, a.K, slot=0, kernels="roll")
     x = torch.zeros(1, device=dev)
+    if flag and a.sched_when == "late":
+        import ctypes
+        print("hipSetDeviceFlags", ctypes.CDLL("libamdhip64.so.7").hipSetDeviceFlags(flag), file=sys.stderr)
     for _ in range(3):   # first uses
         env.replay(1)
         env.replay(0)
@@ -63,7 +74,8 @@ def main():
             out.append((time.perf_counter() - t0) * 1e6)
         return out
 
-    res = {"K": a.K, "N": a.N, "B": a.B, "lib": os.environ.get("GSM_LIB_PATH", "libgsm.so")}
+    res = {"K": a.K, "N": a.N, "B": a.B, "lib": os.environ.get("GSM_LIB_PATH", "libgsm.so"),
+           "sched": a.sched + ("/" + a.sched_when if flag else "")}
     res["sync_only_us"] = med(wall(lambda: None, a.R))
     # the host side of one replay call alone (returns before the kernel runs):
     # GpuBatchEnv.replay (Python, ctypes, current-stream lookup) and the bare
