@@ -41,7 +41,8 @@ def test_counter_bound_classifies():
 def test_committed_lines_fractions_at_most_one():
     """Every committed bench line of the round's package: the counter-based
     shares are at most 1 and agree with counter_bound on the committed PMC."""
-    lines = sorted((ROOT / "profiles" / "r4_lines").glob("bench_*.json"))
+    newest = max((ROOT / "profiles").glob("r*_lines"), key=lambda d: int(d.name[1:].split("_")[0]))
+    lines = sorted(newest.glob("bench_*.json"))
     pmc = json.loads((ROOT / "profiles" / "pmc_kernels.json").read_text())
     assert lines and pmc["entries"]
     seen = 0
