@@ -129,6 +129,7 @@ int align16(int x) { return (x + 15) & ~15; }
 // step against 29.4 for the round-3 weights (profiles/r4_place); padding envs
 // (b >= B) last. roll_place (gsm_ragged_kernels.hip) deals them to the
 // SIMDs in strata.
+constexpr int kXcds = 8;   // MI355X: 8 XCDs of 32 CUs
 int update_block_order(gsm_handle *h, hipStream_t s) {
     const gsm::DevParams &p = h->dp;
     if (p.path != gsm::kPathRagged || p.scenario != gsm::kScnMixed) return GSM_OK;
@@ -161,7 +162,37 @@ int update_block_order(gsm_handle *h, hipStream_t s) {
     for (int k = 0; k < nb; ++k) order[k] = k;
     std::stable_sort(order.begin(), order.begin() + nb, [&](int32_t a, int32_t b) { return key[a] > key[b]; });
     for (int k = 0; k < W; ++k) order[nb + k] = k;
-    std::stable_sort(order.begin() + nb, order.end(), [&](int32_t a, int32_t b) { return cost[a] > cost[b]; });
+    // XCD-local dealing (round 5): roll_place gives SIMD i (XCD-major: the
+    // SIMDs of XCD x are i in [x S/8, (x+1) S/8)) entry i of even strata and
+    // S - 1 - i of odd ones. Each XCD takes a contiguous block of W/8 envs, its
+    // own cost order cut into strata of S/8 and snaked over its SIMDs, so envs
+    // next to each other in memory (their per-env outputs and CSR edges share
+    // cache lines) are written from one XCD's L2 instead of up to eight, each
+    // writing back its own partial copy of the line. GSM_PLACE_XCD=0: one cost
+    // order over the whole grid (round 4).
+    int n_cu = 0, dev = 0;
+    const char *px = getenv("GSM_PLACE_XCD");
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n_cu = 0;
+    const int S = 4 * n_cu, SX = S / kXcds;
+    if (!(px && atoi(px) == 0) && S > 0 && S % kXcds == 0 && W % S == 0) {
+        const int R = W / S, WX = W / kXcds;
+        std::vector<int32_t> blk(WX);
+        for (int x = 0; x < kXcds; ++x) {
+            for (int k = 0; k < WX; ++k) blk[k] = x * WX + k;
+            std::stable_sort(blk.begin(), blk.end(), [&](int32_t a, int32_t b) { return cost[a] > cost[b]; });
+            for (int r = 0; r < R; ++r)
+                for (int il = 0; il < SX; ++il) {
+                    const int i = x * SX + il;                   // the SIMD
+                    const int j = (r & 1) ? S - 1 - i : i;       // its table entry in stratum r
+                    const int e = (r & 1) ? SX - 1 - il : il;    // snaked within the XCD
+                    order[nb + (size_t)r * S + j] = blk[(size_t)r * SX + e];
+                }
+        }
+    } else {
+        std::stable_sort(order.begin() + nb, order.end(), [&](int32_t a, int32_t b) { return cost[a] > cost[b]; });
+    }
     const size_t bytes = (size_t)(nb + W) * sizeof(int32_t);
     hipError_t e = hipSuccess;
     if (!h->block_order) {
@@ -953,7 +984,9 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     }
     const size_t csum_half = one_hop ? (size_t)K * nc * kCsumStride : 0;   // u64
     const size_t pace_words = one_hop ? (size_t)gsm::kPaceKeys * gsm::kPaceStride : 0;   // u32, per half
-    const size_t gran_alloc = 16 + ((size_t)K * (per_wave ? (size_t)(xW + xNG) : (size_t)nb) +
+    // (ragged: the supergroup sums [K][ceil(xNG / 8)] after the group sums)
+    const size_t xNS = ragged ? ((size_t)xNG + gsm::kSupGroups - 1) / gsm::kSupGroups : 0;
+    const size_t gran_alloc = 16 + ((size_t)K * (per_wave ? (size_t)(xW + xNG) + xNS : (size_t)nb) +
                                     2 * csum_half) * sizeof(uint64_t) +
                               2 * pace_words * sizeof(uint32_t) +
                               (ragged ? gsm::PlaceArea::words(xW) * sizeof(uint64_t) : 0);
