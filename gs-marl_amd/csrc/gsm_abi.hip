@@ -984,9 +984,7 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     }
     const size_t csum_half = one_hop ? (size_t)K * nc * kCsumStride : 0;   // u64
     const size_t pace_words = one_hop ? (size_t)gsm::kPaceKeys * gsm::kPaceStride : 0;   // u32, per half
-    // (ragged: the supergroup sums [K][ceil(xNG / 8)] after the group sums)
-    const size_t xNS = ragged ? ((size_t)xNG + gsm::kSupGroups - 1) / gsm::kSupGroups : 0;
-    const size_t gran_alloc = 16 + ((size_t)K * (per_wave ? (size_t)(xW + xNG) + xNS : (size_t)nb) +
+    const size_t gran_alloc = 16 + ((size_t)K * (per_wave ? (size_t)(xW + xNG) : (size_t)nb) +
                                     2 * csum_half) * sizeof(uint64_t) +
                               2 * pace_words * sizeof(uint32_t) +
                               (ragged ? gsm::PlaceArea::words(xW) * sizeof(uint64_t) : 0);

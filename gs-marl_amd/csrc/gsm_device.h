@@ -343,7 +343,6 @@ struct Xfer {
     uint64_t *grp;      // [K][NG]
     uint32_t *status;
     int W, NG;          // waves of the grid, groups of 64 waves
-    int K;              // steps of the launch (the ragged rollout's supergroup sums follow grp)
     uint32_t etag;      // roll_epoch_tag(epoch)
     __device__ __forceinline__ uint32_t tag(int s) const { return etag | (uint32_t)(s + 1); }
 };
@@ -428,48 +427,6 @@ __device__ __forceinline__ void xfer_grp_publish(const Xfer &x, uint64_t l, int 
     const uint32_t v = xfer_settle(l, xfer_grp_addr(x, s, w, lane), lane < 63, tag, x.status);
     const int sum = wave_total((int)v) + own;
     if (lane == 0) xfer_st(x.grp + (int64_t)s * x.NG + (w >> 6), tag, (uint32_t)sum);
-}
-
-// ---- a third level for the ragged rollout (depth >= 3; round 5): supergroups
-// of kSupGroups groups (512 waves). sup[s][u] = the sum of grp[s][8u .. 8u+7],
-// published by the supergroup's last wave in iteration s + 2 (its group sums
-// are published in s + 1). Offset of wave w = sup[s][u' < w / 512] + grp[s][g'
-// in the supergroup, g' < w / 64] + agg[s][group-mates before w]: at C4's 8192
-// waves at most 15 + 7 + 63 granules — 2 + 1 + up to 8 memory requests per
-// wave-step instead of up to 8 + 8 + 8 (the granules are uncached: each
-// request goes to HBM).
-__device__ __forceinline__ int xfer_ns(int NG) { return (NG + kSupGroups - 1) / kSupGroups; }
-__device__ __forceinline__ const uint64_t *xfer_sup_row(const Xfer &x, int s) {
-    return x.grp + (int64_t)x.K * x.NG + (int64_t)s * xfer_ns(x.NG);
-}
-__device__ __forceinline__ XferOff xfer_off_load_h(const Xfer &x, int s, int w, int lane) {
-    const int g = w >> 6, r = w & 63, u = g / kSupGroups, gi = g % kSupGroups;
-    const uint64_t *ag = x.agg + (int64_t)s * x.W + (g << 6);
-    const uint64_t *gg = x.grp + (int64_t)s * x.NG + u * kSupGroups;
-    XferOff o;
-    o.a = xfer_ld(ag + min(lane, r > 0 ? r - 1 : 0));
-    o.g0 = xfer_ld(gg + min(lane, gi > 0 ? gi - 1 : 0));
-    o.g1 = xfer_ld(xfer_sup_row(x, s) + min(lane, u > 0 ? u - 1 : 0));
-    return o;
-}
-__device__ __forceinline__ int xfer_off_settle_h(const Xfer &x, const XferOff &o, int s, int w, int lane) {
-    const int g = w >> 6, r = w & 63, u = g / kSupGroups, gi = g % kSupGroups;
-    const uint32_t tag = x.tag(s);
-    const uint64_t *ag = x.agg + (int64_t)s * x.W + (g << 6);
-    const uint64_t *gg = x.grp + (int64_t)s * x.NG + u * kSupGroups;
-    uint32_t v = xfer_settle(o.a, ag + min(lane, r > 0 ? r - 1 : 0), lane < r, tag, x.status);
-    v += xfer_settle(o.g0, gg + min(lane, gi > 0 ? gi - 1 : 0), lane < gi, tag, x.status);
-    v += xfer_settle(o.g1, xfer_sup_row(x, s) + min(lane, u > 0 ? u - 1 : 0), lane < u, tag, x.status);
-    return wave_total((int)v);
-}
-// by the supergroup's last wave (w % 512 == 511): its 8 group sums of step s
-__device__ __forceinline__ void xfer_sup_publish(const Xfer &x, int s, int w, int lane) {
-    const int u = (w >> 6) / kSupGroups;
-    const uint64_t *gg = x.grp + (int64_t)s * x.NG + u * kSupGroups + min(lane, kSupGroups - 1);
-    const uint32_t tag = x.tag(s);
-    const uint32_t v = xfer_settle(xfer_ld(gg), gg, lane < kSupGroups, tag, x.status);
-    const int sum = wave_total((int)v);
-    if (lane == 0) xfer_st(const_cast<uint64_t *>(xfer_sup_row(x, s)) + u, tag, (uint32_t)sum);
 }
 
 // ---- pacing of the rollouts (round 5; gsm_roll_seg_kernel, gsm_roll_tile_kernel)

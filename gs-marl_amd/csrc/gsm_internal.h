@@ -36,8 +36,6 @@ constexpr int kPaceKeys = 2048, kPaceStride = 16;   // counters, u32 words betwe
 // workgroups per chunk sum of the segmented rollout's one-hop CSR prefix
 // (gsm_device.h roll_prefix)
 constexpr int kPrefixChunk = 64;
-// groups of 64 waves per supergroup of the ragged rollout's hand-off (gsm_device.h)
-constexpr int kSupGroups = 8;
 
 // Everything a launch needs, passed by value (kernarg segment, < 4 KB).
 // fp32 constants are formed on the host exactly as oracle/batch_ref.py:Spec

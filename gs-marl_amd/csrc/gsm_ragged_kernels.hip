@@ -1302,9 +1302,7 @@ __device__ __forceinline__ uint64_t place_ld(const uint64_t *g) {   // a wave-un
            __builtin_amdgcn_readfirstlane((uint32_t)x);
 }
 __device__ __forceinline__ uint64_t *place_area(const KernargParams &q) {
-    // (roll.gran is past the header; then per step the wave counts, the group
-    // sums, the supergroup sums)
-    return q.roll.gran + (int64_t)q.roll.K * (q.roll.xW + q.roll.xNG + xfer_ns(q.roll.xNG));
+    return q.roll.gran + (int64_t)q.roll.K * (q.roll.xW + q.roll.xNG);   // (roll.gran is past the header)
 }
 // Registration counters are spread over kGroups words (XCC x shader engine)
 // so that no word takes more than ~128 atomics per launch.
@@ -1499,7 +1497,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         x.NG = q.roll.xNG;
         x.agg = q.roll.gran;   // (past the allocation's 16-byte header already)
         x.grp = x.agg + (int64_t)q.roll.K * x.W;
-        x.K = q.roll.K;
         x.status = q.roll.status;
         x.etag = roll_epoch_tag(epoch);
         return x;
@@ -1528,13 +1525,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     };
     int ring = 0;                    // k mod (depth + 1): the slab / count of the current step
     const bool glast = (w & 63) == 63;
-    // depth >= 3: the offsets from supergroup sums (gsm_device.h), published by
-    // each supergroup's last wave two iterations after the step
-    const bool hier = D >= 3, slast = (w & (64 * kSupGroups - 1)) == 64 * kSupGroups - 1;
-    auto off_of = [&](const int j) {
-        return hier ? xfer_off_settle_h(xf(), xfer_off_load_h(xf(), j, w, lane), j, w, lane)
-                    : xfer_off_settle(xf(), xfer_off_load(xf(), j, w, lane), j, w, lane);
-    };
     int arow = p.roll.t_first % n_act;
     int cur_edges = 0;              // the env's edge count of the current step
     uint64_t rmask = 0;             // row masks of the current step (collider lanes)
@@ -1677,7 +1667,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         GSM_ACC(late_params(), w, 3, tk0);
         GSM_TNOW(tk1);
         if (k >= 1 && glast) xfer_grp_publish(xf(), xfer_grp_load(xf(), k - 1, w, lane), k - 1, w, lane, cur_edges);
-        if (hier && k >= 2 && slast) xfer_sup_publish(xf(), k - 2, w, lane);
         GSM_ACC(late_params(), w, 5, tk1);
         GSM_TNOW(tk2);
 
@@ -1812,7 +1801,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
         if (k == K - 1 && q.degenerate && lane == 0) {}   // flags written with the final state
         // the edges of step k - depth
         GSM_TNOW(tk4);
-        if (k >= D) pack(k - D, off_of(k - D));
+        if (k >= D) pack(k - D, xfer_off_settle(xf(), xfer_off_load(xf(), k - D, w, lane), k - D, w, lane));
         GSM_ACC(late_params(), w, 7, tk4);
         arow = arow_next;
         ring = ring == D ? 0 : ring + 1;
@@ -1823,7 +1812,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
     for (int k = K; k < K + D; ++k) {
         XferOff xo{0ull, 0ull, 0ull};
         uint64_t xl = 0;
-        if (k >= D) xo = hier ? xfer_off_load_h(xf(), k - D, w, lane) : xfer_off_load(xf(), k - D, w, lane);
+        if (k >= D) xo = xfer_off_load(xf(), k - D, w, lane);
         if (k == K) {
             if (glast) xl = xfer_grp_load(xf(), K - 1, w, lane);
             // block_edge_sum of env block w / 4: its last env adds the others' counts
@@ -1837,9 +1826,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) 
             }
             if (glast) xfer_grp_publish(xf(), xl, K - 1, w, lane, cur_edges);
         }
-        // the supergroup sums of the last two steps
-        if (hier && slast && k - 2 >= 0 && k - 2 < K && k <= K + 1) xfer_sup_publish(xf(), k - 2, w, lane);
-        if (k >= D) pack(k - D, hier ? xfer_off_settle_h(xf(), xo, k - D, w, lane) : xfer_off_settle(xf(), xo, k - D, w, lane));
+        if (k >= D) pack(k - D, xfer_off_settle(xf(), xo, k - D, w, lane));
         ring = ring == D ? 0 : ring + 1;
     }
     // The grid's last wave has read (directly or through the group sums) a
