@@ -1788,7 +1788,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         x.NG = q.roll.xNG;
         x.agg = q.roll.gran;
         x.grp = x.agg + (int64_t)q.roll.K * x.W;
-        x.K = q.roll.K;
         x.status = q.roll.status;
         x.etag = roll_epoch_tag(q.roll.epoch);
         return x;
