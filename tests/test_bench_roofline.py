@@ -41,7 +41,12 @@ def test_counter_bound_classifies():
 def test_committed_lines_fractions_at_most_one():
     """Every committed bench line of the round's package: the counter-based
     shares are at most 1 and agree with counter_bound on the committed PMC."""
-    newest = max((ROOT / "profiles").glob("r*_lines"), key=lambda d: int(d.name[1:].split("_")[0]))
+    import re
+
+    def order(d):   # r5_lines < r5z_lines < r6_lines
+        m = re.match(r"r(\d+)(\w*)_lines$", d.name)
+        return (int(m.group(1)), m.group(2)) if m else (-1, "")
+    newest = max((ROOT / "profiles").glob("r*_lines"), key=order)
     lines = sorted(newest.glob("bench_*.json"))
     pmc = json.loads((ROOT / "profiles" / "pmc_kernels.json").read_text())
     assert lines and pmc["entries"]
