@@ -158,6 +158,34 @@ def test_roll_ragged_episodes_match_chain():
     env.close()
 
 
+def test_roll_ragged_xcd_dealing_same_outputs(monkeypatch):
+    """The placement table only schedules: envs dealt per XCD (contiguous env
+    blocks, the default) and by one cost order over the grid
+    (GSM_PLACE_XCD=0) leave every buffer identical after a full-size C4
+    launch, and both launches are dealt (not the identity fallback)."""
+    B, N, T = 8192, 24, 30
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    out = {}
+    for xcd in ("1", "0"):
+        monkeypatch.setenv("GSM_PLACE_XCD", xcd)   # read when the env draws its shapes (reset)
+        env = _env(scenario="mixed", n_agents=N, n_envs=B, n_agents_min=3, seed=11, episode_length=20)
+        _fresh(env, 11)
+        env.capture(acts, T, slot=0, kernels="roll")
+        env.roll_placement()
+        env.replay(0)
+        torch.cuda.synchronize()
+        assert not env.roll_gave_up()
+        assert env.roll_placement() == (1, 0), xcd
+        out[xcd] = {k: v.clone() for k, v in env.t.items()}
+        env.close()
+    ref = out["0"]
+    for k in KEYS:
+        assert torch.equal(ref[k], out["1"][k]), k
+    n = int(ref["edge_ptr"][-1])
+    assert torch.equal(ref["edge_index"][:, :n], out["1"]["edge_index"][:, :n])
+    assert torch.equal(ref["edge_attr"][:n], out["1"]["edge_attr"][:n])
+
+
 @pytest.mark.parametrize("scenario,N,B", [("mixed", 24, 96), ("polygon", 10, 40), ("line", 7, 40)])
 def test_roll_ragged_last_step_oracle(scenario, N, B):
     """The last step of a rollout launch vs oracle/ragged_ref.py stepped from
