@@ -1206,7 +1206,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     // positions before step j, by j % 3
     auto pos_buf = [&](int j3) { return (float2 *)(wave_lds + (j3 == 0 ? 0 : kStep + (j3 - 1) * 8 * E)); };
     int *s_bc = (int *)(smem + kWavesPerBlock * wstride);   // [3][waves]: per-env edge counts by step % 3
-    int *s_red = s_bc + 3 * kWavesPerBlock;                 // [4]: the workgroup's offset, pace counter, rank, pad
+    int *s_red = s_bc + 3 * kWavesPerBlock;                 // [4]: the workgroup's offset, pace level, rank, pad
     int *s_pre = s_red + 4;                                 // [3][waves]: exclusive prefix of the counts
     constexpr int scr_cap = (kStep - 8 * E) / 4;
     const bool wave_live = L0.b < p.B;
@@ -1307,9 +1307,14 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             const int cs = qe.roll.csum_stride;
             const int ex = roll_prefix(qe.roll.gran + (int64_t)j * gridDim.x, qe.roll.csum + (int64_t)j * nc * cs, cs,
                                        etag | (uint32_t)(j + 1), qe.roll.status, L.lane);
+            // the pace level formed here once for the workgroup (wave-uniform
+            // SALU work that every wave repeated before)
+            const int lvl = done > 0 ? pace_level((uint32_t)__builtin_amdgcn_readfirstlane(pv), done,
+                                                  __builtin_amdgcn_readfirstlane(s_red[2]), qe.roll.pace_q)
+                                     : 1;
             if (L.lane == 0) {
                 s_red[0] = ex;
-                s_red[1] = (int)pv;
+                s_red[1] = lvl;
             }
         }
         GSM_ACC(p, L.b, 12, te1);   // the prefix (wave 0)
@@ -1317,9 +1322,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         __syncthreads();
         GSM_ACC(p, L.b, 13, te2);   // waiting for it
         GSM_TNOW(te3);
-        if (done > 0)
-            pace_set(pace_level((uint32_t)__builtin_amdgcn_readfirstlane(s_red[1]), done,
-                                __builtin_amdgcn_readfirstlane(s_red[2]), late_params().roll.pace_q));
+        if (done > 0) pace_set(__builtin_amdgcn_readfirstlane(s_red[1]));
         // (the prefix formed once by thread 0, not w < wave selects: those
         // are loop-invariant lane masks the compiler holds in SGPR pairs)
         const int before = s_pre[cj3 * kWavesPerBlock + wave];

@@ -898,8 +898,13 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                 ex = roll_prefix(q.roll.gran + (int64_t)(k - 2) * gridDim.x, q.roll.csum + (int64_t)(k - 2) * nc * cs,
                                  cs, etag | (uint32_t)(k - 1), q.roll.status, lane);
             }
+            // the pace level formed once here for the workgroup (it was the
+            // same wave-uniform SALU work repeated by all eight waves)
+            const int lvl = k < K && pacing() ? pace_level((uint32_t)__builtin_amdgcn_readfirstlane(pv), k,
+                                                            __builtin_amdgcn_readfirstlane(s_x[3]), q.roll.pace_q)
+                                              : 0;   // (the tail: level 0, as pace_level of a zero counter)
             if (lane == 0) {
-                s_x[1] = (int)pv;
+                s_x[1] = lvl;
                 // (an offset past the capacity is a legal overflow of a small
                 // slot: edge_ptr keeps it, emit_env stops its writes at the
                 // capacity)
@@ -972,9 +977,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         __syncthreads();
         // this workgroup's pace level (from the counter the last wave loaded
         // at the top of the iteration, published by the barrier above)
-        if (k > 0 && pacing())
-            pace_set(pace_level((uint32_t)__builtin_amdgcn_readfirstlane(s_x[1]), k,
-                                __builtin_amdgcn_readfirstlane(s_x[3]), late_params().roll.pace_q));
+        if (k > 0 && pacing()) pace_set(__builtin_amdgcn_readfirstlane(s_x[1]));
         for (int i = tid; i < N; i += kTileBlock) s_pos[i] = s_np[i];
         __syncthreads();
         t += 1;
