@@ -579,6 +579,25 @@ __device__ __forceinline__ void write_staged(const Lane &L, const float2 *s_pos,
     constexpr int E = 2 * kN + kNo;
     const int64_t eb = L.b;
     const int32_t g0 = (int32_t)(eb * E);
+    if (out.cap < ((int64_t)1 << 29)) {
+        // SGPR base (the sink's arrays) + 32-bit VGPR byte offset (the env's
+        // offset and the edge): no 64-bit scalar address arithmetic per env
+        // (8 * cap < 2^32 bytes)
+        const uint32_t wb = (uint32_t)env_off, cap4 = (uint32_t)out.cap * 4u;
+        char *const isrc = (char *)out.index, *const attr = (char *)out.attr;
+        for (int e = L.lane; e < total; e += kWave) {
+            const uint32_t w = s_scr[e];
+            const uint32_t a = w & 0xffu, b = w >> 8;
+            const float2 pa = s_pos[a], pb = s_pos[b];
+            const float dx = pa.x - pb.x, dy = pa.y - pb.y;
+            uint32_t byte = (wb + (uint32_t)e) << 2;
+            asm("" : "+v"(byte));   // keeps the stores in SGPR-base + 32-bit-offset form
+            *(int32_t *)(isrc + byte) = g0 + (int32_t)a;
+            *(int32_t *)(isrc + (byte + cap4)) = g0 + (int32_t)b;
+            *(float *)(attr + byte) = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+        }
+        return;
+    }
     const uint32_t wb_lo = __builtin_amdgcn_readfirstlane((uint32_t)env_off);
     const uint32_t wb_hi = __builtin_amdgcn_readfirstlane((uint32_t)((uint64_t)env_off >> 32));
     const int64_t wbase = (int64_t)(((uint64_t)wb_hi << 32) | wb_lo);
@@ -590,7 +609,7 @@ __device__ __forceinline__ void write_staged(const Lane &L, const float2 *s_pos,
         const float2 pa = s_pos[a], pb = s_pos[b];
         const float dx = pa.x - pb.x, dy = pa.y - pb.y;
         uint32_t byte = (uint32_t)e << 2;
-        asm("" : "+v"(byte));   // keeps the stores in SGPR-base + 32-bit-offset form
+        asm("" : "+v"(byte));
         *(int32_t *)(isrc + byte) = g0 + (int32_t)a;
         *(int32_t *)(idst + byte) = g0 + (int32_t)b;
         *(float *)(attr + byte) = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
@@ -1433,9 +1452,12 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         const int ci = L.agent ? ccnt : 0;
         const int csum = wave_total(ci);
         if (L.agent) {
+            // (32-bit byte offsets from the kernarg base: SGPR base + VGPR
+            // offset stores, no 64-bit scalar address arithmetic per store)
             KernargParams &q = late_params();
-            (q.ro.rew + (kSlots ? k * q.ro.rc_s : 0) + eb * N)[um] = q.shared_reward ? rsum : r;
-            (q.ro.cost + (kSlots ? k * q.ro.rc_s : 0) + eb * N)[um] = (float)ci;
+            const uint32_t off = ((uint32_t)eb * (uint32_t)N + um) * 4u;
+            *(float *)((char *)(q.ro.rew + (kSlots ? k * q.ro.rc_s : 0)) + off) = q.shared_reward ? rsum : r;
+            *(float *)((char *)(q.ro.cost + (kSlots ? k * q.ro.rc_s : 0)) + off) = (float)ci;
         }
         if (late_params().shared_reward) rsum *= (float)N;
         if (L.live) {
@@ -1487,16 +1509,24 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         // the loop
         KernargParams &q = late_params();
         const bool any_statics = q.nf_full || __any(relaid);
-        if (L.live) {
-            float *nf = q.ro.nf + (kSlots ? k * q.ro.nf_s : 0) + eb * E * 7;
-            if (L.agent) {
-                const float2 g = s_pos[N + m];
-                store_row(nf + m * 7, v, pm, make_float2(g.x - pm.x, g.y - pm.y), 0.0f);
-                if (any_statics)
-                    store_row(nf + (N + m) * 7, make_float2(0.0f, 0.0f), g, make_float2(0.0f, 0.0f), 1.0f);
-            } else if (any_statics) {
-                store_row(nf + (N + m) * 7, make_float2(0.0f, 0.0f), pm, make_float2(0.0f, 0.0f), 2.0f);
-            }
+        {
+            // one store block per row kind, its values selected by bit masks
+            // (plain VALU; nested lane branches cost ~20 exec-mask SALU per
+            // step): agent lanes their agent row (v, p, goal - p, 0), obstacle
+            // lanes with statics their obstacle row (0, p, 0, 2) — v is 0
+            // there — then agent lanes with statics their goal row (0, goal, 0, 1)
+            const uint32_t am = (uint32_t)((int)(um - (uint32_t)N) >> 31);   // ~0 on agent lanes
+            const float2 g = s_pos[N + (um & am)];
+            const float2 gr = make_float2(__uint_as_float(__float_as_uint(g.x - pm.x) & am),
+                                          __uint_as_float(__float_as_uint(g.y - pm.y) & am));
+            const float type = __uint_as_float(~am & 0x40000000u);           // 0 or 2
+            char *nfb = (char *)(q.ro.nf + (kSlots ? k * q.ro.nf_s : 0));
+            const uint32_t env_el = (uint32_t)eb * (uint32_t)(E * 7);
+            if (L.live && (L.agent || any_statics))
+                store_row((float *)(nfb + (env_el + (um + (~am & (uint32_t)N)) * 7u) * 4u), v, pm, gr, type);
+            if (L.agent && any_statics)
+                store_row((float *)(nfb + (env_el + (um + (uint32_t)N) * 7u) * 4u), make_float2(0.0f, 0.0f), g,
+                          make_float2(0.0f, 0.0f), 1.0f);
         }
         if (k == K - 1 && q.degenerate) {
             const uint64_t nb = __ballot(L.agent && nonfinite2(pm));
