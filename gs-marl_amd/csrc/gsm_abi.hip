@@ -834,6 +834,11 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     if (flags & ~(GSM_GRAPH_ROLL | GSM_GRAPH_TIME_ENDS))
         return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL combines with GSM_GRAPH_TIME_ENDS only");
     if (!actions || n_actions < 1 || stride < 0) return fail(h, GSM_EINVAL, "bad capture arguments");
+    // the rollout kernels address the action rows with 32-bit byte offsets
+    if ((uint64_t)n_actions * (uint64_t)stride >= ((uint64_t)1 << 32)) {
+        if (fallback) return kRollIneligible;
+        return fail(h, GSM_EINVAL, "GSM_GRAPH_ROLL: the action rows must span < 4 GiB");
+    }
     if (n_steps < 1) return fail(h, GSM_EINVAL, "n_steps must be >= 1");
     if (action_fmt < GSM_ACT_ONEHOT || action_fmt > GSM_ACT_CONT) return fail(h, GSM_EINVAL, "bad action_fmt");
     gsm::DevParams p = h->dp;

@@ -1149,17 +1149,19 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
 // all 8 waves per SIMD resident (2048 workgroups at 8192 envs: one residency round)
 #define GSM_ROLL_ATTR __attribute__((amdgpu_waves_per_eu(8, 8)))
 // a lane's action of the given step row, as loaded (decoded by roll_force)
+// (32-bit byte offsets from the kernarg base: capture_roll requires the
+// action rows to span < 2^32 bytes, so no 64-bit scalar arithmetic per step)
 template <int kN, int kFmt, typename Params>   // DevParams or its kernarg view
 __device__ __forceinline__ float4 roll_action_load(const Params &p, int row, int64_t eb, uint32_t ma) {
-    const char *base = p.roll.actions + (int64_t)row * p.roll.stride;
-    const int64_t ai = eb * kN + ma;
+    const char *base = p.roll.actions;
+    const uint32_t rb = (uint32_t)row * (uint32_t)p.roll.stride, ai = (uint32_t)eb * (uint32_t)kN + ma;
     if constexpr (kFmt == 0) {
-        const float *q = (const float *)base + ai * 5;
+        const float *q = (const float *)(base + (rb + ai * 20u));
         return make_float4(q[1], q[2], q[3], q[4]);
     } else if constexpr (kFmt == 1) {
-        return make_float4(__int_as_float(((const int32_t *)base)[ai]), 0.0f, 0.0f, 0.0f);
+        return make_float4(__int_as_float(*(const int32_t *)(base + (rb + ai * 4u))), 0.0f, 0.0f, 0.0f);
     } else {
-        const float2 a = ((const float2 *)base)[ai];
+        const float2 a = *(const float2 *)(base + (rb + ai * 8u));
         return make_float4(a.x, a.y, 0.0f, 0.0f);
     }
 }
@@ -1180,11 +1182,13 @@ __device__ __forceinline__ float2 roll_force(const Params &p, float4 a, bool age
     return agent ? make_float2(ux * p.sens, uy * p.sens) : make_float2(0.0f, 0.0f);
 }
 
-// LDS per wave of the segmented rollout: [positions E | staging scratch 28 E]
-// rounded to 16 B, then [positions E][positions E][next forces N][row masks
-// of 64 lanes]
-constexpr int roll_lds_step(int E) { return (36 * E + 15) & ~15; }
-constexpr int roll_lds_wave(int N, int E) { return roll_lds_step(E) + 16 * E + 8 * N + 8 * kWave; }
+// LDS per wave of the segmented rollout: [positions E][positions E][positions
+// E] rounded to 16 B, [staging scratch 28 E] rounded to 16 B, [next forces N]
+// [row masks of 64 lanes]. Buffer j at j * 8 E: one multiply per use (a select
+// between two bases cost four scalar instructions per use).
+constexpr int roll_lds_scr(int E) { return (24 * E + 15) & ~15; }
+constexpr int roll_lds_force(int E) { return roll_lds_scr(E) + ((28 * E + 15) & ~15); }
+constexpr int roll_lds_wave(int N, int E) { return roll_lds_force(E) + 8 * N + 8 * kWave; }
 
 // kSlots: per-step outputs at base + k * stride (a rollout buffer); else every
 // step into the bound buffers (the strides are 0 and fold away)
@@ -1211,23 +1215,23 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     // and writes the agents' new positions into buffer (k + 1) % 3, so the
     // positions after step k - 2, which iteration k emits the edges of, are
     // still in the third; goals and obstacles (static within an episode) are
-    // kept in all three. Compile-time layout (roll_kernel_lds): [positions |
-    // staging scratch], [positions], [positions], [the next step's agent
-    // forces], [the row masks of step k - 2].
-    constexpr int kStep = roll_lds_step(E), wstride = roll_lds_wave(N, E);
+    // kept in all three. Compile-time layout (roll_kernel_lds): [positions] x 3,
+    // [staging scratch], [the next step's agent forces], [the row masks of
+    // step k - 2].
+    constexpr int wstride = roll_lds_wave(N, E);
     unsigned char *wave_lds = smem + wave * wstride;
     float2 *const s_buf0 = (float2 *)wave_lds;
-    float *s_nf = (float *)(s_buf0 + E);
-    float2 *const s_buf1 = (float2 *)(wave_lds + kStep);
+    float2 *const s_buf1 = s_buf0 + E;
     float2 *const s_buf2 = s_buf1 + E;
-    float2 *s_force = s_buf2 + E;
+    float *s_nf = (float *)(wave_lds + roll_lds_scr(E));
+    float2 *s_force = (float2 *)(wave_lds + roll_lds_force(E));
     uint64_t *const s_row = (uint64_t *)(s_force + N);
     // positions before step j, by j % 3
-    auto pos_buf = [&](int j3) { return (float2 *)(wave_lds + (j3 == 0 ? 0 : kStep + (j3 - 1) * 8 * E)); };
+    auto pos_buf = [&](int j3) { return s_buf0 + j3 * E; };
     int *s_bc = (int *)(smem + kWavesPerBlock * wstride);   // [3][waves]: per-env edge counts by step % 3
     int *s_red = s_bc + 3 * kWavesPerBlock;                 // [4]: the workgroup's offset, pace level, rank, pad
     int *s_pre = s_red + 4;                                 // [3][waves]: exclusive prefix of the counts
-    constexpr int scr_cap = (kStep - 8 * E) / 4;
+    constexpr int scr_cap = 7 * E;   // words of staging scratch
     const bool wave_live = L0.b < p.B;
     const int64_t eb = wave_live ? L0.b : 0;
     GSM_RSTAMP(p, L0.b, 0);   // diagnostic builds: the launch's timeline per wave
