@@ -281,7 +281,10 @@ int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream);
  * capacity, allocated on first use, since a workgroup may trail its
  * successors by steps). Combines with GSM_GRAPH_TIME_ENDS only (the events
  * then bracket the launch: gsm_graph_kernel_ms gives its time per step);
- * GSM_EINVAL where the config has no rollout kernel. */
+ * GSM_EINVAL where the config has no rollout kernel, or where the action rows
+ * span 4 GiB or more (n_actions * action_stride_bytes >= 2^32: the rollout
+ * kernels address them with 32-bit offsets; without GSM_GRAPH_ROLL such a
+ * capture takes the per-step chain). */
 #define GSM_GRAPH_ROLL 64
 int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t action_stride_bytes,
                       int32_t n_actions, int32_t n_steps, int action_fmt, int flags);
