@@ -355,6 +355,26 @@ def test_eager_one_launch_redirected_outputs(N, B, monkeypatch):
         assert torch.equal(a["edge_attr"][:n], b["edge_attr"][:n]), t
 
 
+def test_roll_capture_refuses_action_rows_past_4gib():
+    """The rollout kernels address the action rows with 32-bit byte offsets:
+    an explicit GSM_GRAPH_ROLL capture whose rows span 4 GiB or more is
+    refused (GSM_EINVAL) before anything is launched; the default capture
+    takes the per-step chain instead (no launch here either: nothing replays)."""
+    import ctypes as C
+
+    from gsmarl_amd import _lib
+    env, _ = _env(n_agents=24, n_envs=64, episode_length=4)
+    acts = torch.zeros((2, 64, 24), dtype=torch.int32, device=DEV)
+    ptr = C.c_void_p(acts.data_ptr())
+    rc = env.lib.gsm_graph_capture(env._h, 0, ptr, 1 << 31, 2, 2, _lib.ACT_INDEX, _lib.GRAPH_ROLL)
+    assert rc == _lib.GSM_EINVAL
+    assert "4 GiB" in _lib.last_error(env.lib, env._h)
+    rc = env.lib.gsm_graph_capture(env._h, 0, ptr, 1 << 31, 2, 2, _lib.ACT_INDEX, 0)
+    assert rc == _lib.GSM_OK, _lib.last_error(env.lib, env._h)
+    assert not env.graph_is_rollout(0)
+    env.close()
+
+
 def test_roll_replay_refused_inside_stream_capture():
     """A rollout graph takes its own hand-off epoch and its half of the chunk-
     sum double buffer at every launch, so a launch recorded into the caller's
