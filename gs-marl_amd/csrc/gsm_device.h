@@ -470,6 +470,16 @@ __device__ __forceinline__ void pace_set(int lvl) {   // lvl wave-uniform
         __builtin_amdgcn_s_setprio(2);
 }
 
+// the priority of a rollout's first iterations, before the pace levels take
+// over (gsm_roll_seg_kernel; -DGSM_START_PRIO=0: none, the A/B baseline)
+#ifndef GSM_START_PRIO
+#define GSM_START_PRIO 1
+#endif
+template <int kLvl>
+__device__ __forceinline__ void start_prio() {
+    if constexpr (GSM_START_PRIO != 0) __builtin_amdgcn_s_setprio(kLvl);
+}
+
 // ---- one-hop CSR prefix of the one-env-per-wave segmented rollout (round 5)
 // The packed offset of workgroup w's edges of step s is the sum of the edge
 // counts of every workgroup before it. Two kinds of words per step:

@@ -1237,6 +1237,13 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     GSM_RSTAMP(p, L0.b, 0);   // diagnostic builds: the launch's timeline per wave
     GSM_SET(p, L0.b, 9, (uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 4) |                  // HW_ID
                             ((uint64_t)__builtin_amdgcn_s_getreg((31 << 11) | 20) << 32));   // XCC_ID
+    // start priorities (the pace levels take over from iteration 2): the
+    // entry at 3, so that a late workgroup's state loads issue at once; step 0
+    // at 2 and step 1 at 1, so that no wave runs a later step while one on its
+    // SIMD is still in an earlier one — oldest-first issue alone let a CU's
+    // rank-0 workgroup finish step 0 at 4.9 us and rank 7 at 21.5 us, and
+    // iteration 2's emission waits for step 0 of every workgroup
+    start_prio<3>();
     // pacing: this workgroup's CU counter (the arrival now, a step after each
     // step; its address re-formed at each use, no SGPRs held across the loop),
     // and the counters of the slot's next launch zeroed
@@ -1275,6 +1282,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     }
     if (threadIdx.x == 0) s_red[2] = (int)(pace_v >> 24);   // the rank on the CU (its load waited above)
     wave_sync();
+    start_prio<2>();
     GSM_RSTAMP(p, L0.b, 1);
     // apply_environment_force: the action force plus the contact terms of the
     // candidates in ascending collider order
@@ -1603,6 +1611,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         // next iteration's emission)
         if (threadIdx.x == 0 && pacing())
             (void)__hip_atomic_fetch_add(pace_ctr(), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (k == 0) start_prio<1>();
         // keep step t - 1's row masks for the next iteration's emission and
         // step t's for its sweep
         s_row[L.lane] = oo;
