@@ -1053,11 +1053,15 @@ __global__ __launch_bounds__(kBlock) void gsm_step_seg_kernel(DevParams p) {
     int *s_lag = s_bc + kWavesPerBlock;
     GSM_RSTAMP(p, wid, 8);
     GSM_STAMP(p, wid, 0);
+    // (the loads issued at priority 3: a late workgroup's state requests go
+    // out at once instead of after the older waves' compute, then 1)
+    start_prio<3>();
     {
         SegIn in{};
         if constexpr (kG == 1) in = seg_load<kN, kNo, kFmt, kLag>(p, s, L);
         BlockPrefix lag_pre{0, 0};
         if constexpr (kLag) lag_pre = block_prefix_loads(p.lag.block_sum, p.lag.edge_count, p.B, s.G, p.pos);
+        start_prio<1>();
         const int edges = seg_env<kN, kNo, kFmt, kLag>(p, s, L, wave_lds, in, wid, lag_pre, s_lag);
         if (L.lane == 0) s_bc[wave] = edges;
         __syncthreads();
@@ -1089,7 +1093,9 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
     GSM_STAMP(p, wid, 0);
 
     // every global load first (positions, row masks, the block's edge counts,
-    // the preceding blocks' sums), then the first wait
+    // the preceding blocks' sums; at priority 3, as in the step kernel), then
+    // the first wait
+    start_prio<3>();
     const BlockPrefix pre = block_prefix_loads(p.block_edge_sum, p.edge_count, p.B, G, p.pos);
     uint64_t mask = 0;
     float2 x0 = make_float2(0.0f, 0.0f), x1 = x0;
@@ -1103,6 +1109,7 @@ __global__ __launch_bounds__(kBlock) void gsm_emit_seg_kernel(DevParams p) {
     } else if (L.live) {
         mask = p.row_mask[eb * M + m];
     }
+    start_prio<1>();
     if constexpr (kG == 1) {
         if (L.b < p.B) {
             if (L.lane < E) s_pos[L.lane] = x0;
@@ -1635,17 +1642,9 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         r3 = r3n;
         wave_sync();
     }
-    {   // the tail: the last two steps' edges (r3 = K % 3)
-        Lane L = L0;
-        asm volatile("" : "+v"(L.lane), "+v"(L.m));
-        GSM_RSTAMP(p, L.b, 5);
-        const int rm1 = r3 == 0 ? 2 : r3 - 1;   // (K - 1) % 3
-        if (K >= 2) emit_step(K - 2, rm1, rm1 == 0 ? 2 : rm1 - 1, s_row[L.lane], 0, L);
-        GSM_RSTAMP(p, L.b, 6);
-        emit_step(K - 1, r3, rm1, oo, 0, L);
-        GSM_RSTAMP(p, L.b, 7);
-    }
-    // the final state (what the next launch or an eager step reads)
+    // the final state (what the next launch or an eager step reads), stored
+    // before the tail: its emissions wait for the last steps' offsets, and
+    // these stores need none
     KernargParams &q = late_params();
     if (wave_live) {
         float2 *const pos_b = q.pos + eb * E;
@@ -1663,6 +1662,16 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             q.ep_acc[L0.b] = acc;
             if (q.degenerate) q.degenerate[L0.b] = deg;
         }
+    }
+    {   // the tail: the last two steps' edges (r3 = K % 3)
+        Lane L = L0;
+        asm volatile("" : "+v"(L.lane), "+v"(L.m));
+        GSM_RSTAMP(p, L.b, 5);
+        const int rm1 = r3 == 0 ? 2 : r3 - 1;   // (K - 1) % 3
+        if (K >= 2) emit_step(K - 2, rm1, rm1 == 0 ? 2 : rm1 - 1, s_row[L.lane], 0, L);
+        GSM_RSTAMP(p, L.b, 6);
+        emit_step(K - 1, r3, rm1, oo, 0, L);
+        GSM_RSTAMP(p, L.b, 7);
     }
     GSM_RSTAMP(p, L0.b, 8);
 }
