@@ -471,18 +471,72 @@ hipError_t gran_malloc(void **base, uint64_t **gran, size_t bytes) {
     return hipSuccess;
 }
 
-// gsm_step as ONE launch (opt-in, GSM_EAGER_ONE_LAUNCH=1): the config's fused
-// rollout kernel with K = 1 (the step, then its edges at the CSR offset of the
-// in-launch look-back) instead of the step kernel + the emit kernel — the same
-// operations, so the same outputs (tests/test_gpu_roll.py). Segmented configs
-// with a compiled rollout shape and the tile path, when the grid fits one
-// residency round (decided once per handle); the ragged path keeps its two
-// launches. Not the default: measured slower at H, 28.6 vs 18.7 us per step
-// (DESIGN.md §4): in one launch every wave runs the same phase at once, and the
-// last workgroup's look-back waits for the slowest of all the others' steps
-// (profiles/r4_stamps/stamps_h.json).
+// gsm_step as ONE launch: the config's fused rollout kernel with K = 1 (the
+// step, then its edges at the CSR offset of the in-launch prefix) instead of
+// the step kernel + the emit kernel — the same operations, so the same outputs
+// (tests/test_gpu_roll.py), when the grid fits one residency round (decided
+// once per handle). The default for the one-env-per-wave segmented rollout
+// (navigation with 6, 12 or 24 agents: 15.4 vs 16.5 us per step at H, 13.1 vs
+// 15.5 at 12 x 8192; DESIGN.md §4, profiles/r5_ab/eager_forms); the packed
+// small-env and tile rollouts keep the two launches unless
+// GSM_EAGER_ONE_LAUNCH=1 (there the pair was faster: C2 8.7 vs 9.4, C3 27.9
+// vs 29.6 us), and GSM_EAGER_ONE_LAUNCH=0 keeps them everywhere. The ragged
+// path always runs two launches.
 constexpr int kEagerIneligible = 1;
+// Decided once per handle, at gsm_bind (the hand-off granules allocated and
+// zeroed there, so that no step allocates or synchronises): h->eager_roll 1
+// when the config has a rollout kernel whose grid fits one residency round
+// and the one launch is wanted (above), else 0.
+int eager_setup(gsm_handle *h) {
+    gsm::DevParams p = h->dp;
+    p.action_fmt = GSM_ACT_INDEX;   // (every format's kernel has the same LDS and occupancy)
+    h->eager_roll = 0;
+    if (p.path == gsm::kPathRagged) return GSM_OK;
+    const bool tile = p.path == gsm::kPathTile;
+    const void *fn = tile ? gsm::roll_tile_kernel_fn(p, false) : gsm::roll_seg_kernel_fn(p, false);
+    if (!fn) return GSM_OK;
+    const int per_blk = tile ? 1 : gsm::roll_seg_envs_per_block(p);
+    const int nb = tile ? gsm::step_grid_blocks(p) : (p.B + per_blk - 1) / per_blk;
+    const size_t lds = tile ? gsm::roll_tile_kernel_lds(p) : gsm::roll_kernel_lds(p);
+    const char *ev = getenv("GSM_EAGER_ONE_LAUNCH");
+    const bool want = ev && *ev ? atoi(ev) != 0 : !tile && !gsm::roll_packed(p);
+    if (!want) return GSM_OK;
+    int dev = 0, per_cu = 0, n_cu = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, gsm::block_threads(p), lds);
+    if (e != hipSuccess) return hip_fail(h, e, "occupancy query (eager rollout)");
+    if ((int64_t)per_cu * n_cu < nb) return GSM_OK;
+    // (tile path: aggregates + inclusive prefixes per workgroup;
+    // segmented: aggregates + two halves of chunk sums; packed small envs:
+    // per-wave counts + group sums)
+    const size_t xw = (size_t)nb * gsm::kWavesPerBlock;
+    const size_t nc = ((size_t)nb + gsm::kPrefixChunk - 1) / gsm::kPrefixChunk;
+    const size_t words = std::max({2 * (size_t)nb, (size_t)nb + 2 * nc * kCsumStride,
+                                   xw + (xw + gsm::kWave - 1) / gsm::kWave});
+    const size_t bytes = 16 + words * sizeof(uint64_t);
+    e = gran_malloc(&h->eager_base, &h->eager_gran, bytes);
+    h->eager_gran_end = h->eager_gran ? (uint64_t *)((char *)h->eager_gran + bytes) : nullptr;
+    h->eager_csum = h->eager_gran ? h->eager_gran + 2 + nb : nullptr;
+    h->eager_csum_half = (int64_t)(nc * kCsumStride);
+    if (e != hipSuccess) { h->eager_gran = nullptr; return hip_fail(h, e, "hipMalloc (eager granules)"); }
+    e = gsm::launch_granule_init(h->eager_gran, bytes, 0u, nullptr);
+    if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    if (e == hipSuccess && !h->roll_status) {
+        e = hipMalloc(&h->roll_status, 16);
+        if (e == hipSuccess) e = clear_status(h);
+        if (e != hipSuccess) h->roll_status = nullptr;
+    }
+    if (e != hipSuccess) return hip_fail(h, e, "eager rollout setup");
+    h->eager_roll = 1;
+    return GSM_OK;
+}
+
 int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
+    if (h->eager_roll < 0) {   // (gsm_bind decides it; kept for a handle bound before)
+        const int rc = eager_setup(h);
+        if (rc) return rc;
+    }
     if (h->eager_roll == 0 || p.path == gsm::kPathRagged) return kEagerIneligible;
     // a stream being captured into a graph (e.g. torch.cuda.graph around a
     // policy + env.step): the two launches, which hold no per-launch state —
@@ -495,41 +549,6 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
     const int per_blk = tile ? 1 : gsm::roll_seg_envs_per_block(p);
     const int nb = tile ? gsm::step_grid_blocks(p) : (p.B + per_blk - 1) / per_blk;
     const size_t lds = tile ? gsm::roll_tile_kernel_lds(p) : gsm::roll_kernel_lds(p);
-    if (h->eager_roll < 0) {
-        h->eager_roll = 0;
-        const char *ev = getenv("GSM_EAGER_ONE_LAUNCH");
-        if (!ev || atoi(ev) == 0) return kEagerIneligible;
-        int dev = 0, per_cu = 0, n_cu = 0;
-        hipError_t e = hipGetDevice(&dev);
-        if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-        if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, gsm::block_threads(p), lds);
-        if (e != hipSuccess) return hip_fail(h, e, "occupancy query (eager rollout)");
-        if ((int64_t)per_cu * n_cu < nb) return kEagerIneligible;
-        // (look-back: aggregates + inclusive prefixes per workgroup; packed
-        // small envs: per-wave counts + group sums)
-        // (tile path: aggregates + inclusive prefixes per workgroup;
-        // segmented: aggregates + two halves of chunk sums; packed small envs:
-        // per-wave counts + group sums)
-        const size_t xw = (size_t)nb * gsm::kWavesPerBlock;
-        const size_t nc = ((size_t)nb + gsm::kPrefixChunk - 1) / gsm::kPrefixChunk;
-        const size_t words = std::max({2 * (size_t)nb, (size_t)nb + 2 * nc * kCsumStride,
-                                       xw + (xw + gsm::kWave - 1) / gsm::kWave});
-        const size_t bytes = 16 + words * sizeof(uint64_t);
-        e = gran_malloc(&h->eager_base, &h->eager_gran, bytes);
-        h->eager_gran_end = h->eager_gran ? (uint64_t *)((char *)h->eager_gran + bytes) : nullptr;
-        h->eager_csum = h->eager_gran ? h->eager_gran + 2 + nb : nullptr;
-        h->eager_csum_half = (int64_t)(nc * kCsumStride);
-        if (e != hipSuccess) { h->eager_gran = nullptr; return hip_fail(h, e, "hipMalloc (eager granules)"); }
-        e = gsm::launch_granule_init(h->eager_gran, bytes, 0u, nullptr);
-        if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
-        if (e == hipSuccess && !h->roll_status) {
-            e = hipMalloc(&h->roll_status, 16);
-            if (e == hipSuccess) e = clear_status(h);
-            if (e != hipSuccess) h->roll_status = nullptr;
-        }
-        if (e != hipSuccess) return hip_fail(h, e, "eager rollout setup");
-        h->eager_roll = 1;
-    }
     // the step's outputs: the bound (or redirected) buffers, its edges too
     p.ro = gsm::DevParams::RollOut{p.node_feat, p.reward, p.cost, p.done, p.edge_count, p.edge_ptr, p.edge_index,
                                    p.edge_attr, 0, 0, 0, 0, 0, 0, 0, p.edge_capacity, nullptr, nullptr, p.assign, 0};
@@ -723,6 +742,7 @@ int gsm_bind(gsm_handle *h, const gsm_buffers *b) {
     p.lsa_stats = b->lsa_stats;
     h->bound = true;
     drop_graph(h);   // a captured graph holds the old pointers
+    if (h->eager_roll < 0) return eager_setup(h);
     return GSM_OK;
 }
 

@@ -295,15 +295,16 @@ def test_roll_recycled_after_many_replays():
 @pytest.mark.parametrize("N,B", [(24, 8192), (3, 4096), (96, 1024), (12, 100), (6, 37)])
 def test_eager_one_launch_equals_two_kernels(N, B, monkeypatch):
     """gsm_step as one rollout launch of one step (GSM_EAGER_ONE_LAUNCH=1,
-    where the config has a rollout kernel) leaves every buffer exactly as the
-    default step kernel + emit kernel pair does, over steps with auto-resets,
+    where the config has a rollout kernel; the default at 6-24 agents) leaves
+    every buffer exactly as the step kernel + emit kernel pair
+    (GSM_EAGER_ONE_LAUNCH=0) does, over steps with auto-resets,
     in both the bound buffers and redirected outputs."""
     T, EL = 7, 5
     acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
     envs = []
     for two in (True, False):
         if two:
-            monkeypatch.delenv("GSM_EAGER_ONE_LAUNCH", raising=False)
+            monkeypatch.setenv("GSM_EAGER_ONE_LAUNCH", "0")
         else:
             monkeypatch.setenv("GSM_EAGER_ONE_LAUNCH", "1")
         env, _ = _env(n_agents=N, n_envs=B, episode_length=EL, seed=9)
@@ -331,7 +332,7 @@ def test_eager_one_launch_redirected_outputs(N, B, monkeypatch):
     got = []
     for two in (True, False):
         if two:
-            monkeypatch.delenv("GSM_EAGER_ONE_LAUNCH", raising=False)
+            monkeypatch.setenv("GSM_EAGER_ONE_LAUNCH", "0")
         else:
             monkeypatch.setenv("GSM_EAGER_ONE_LAUNCH", "1")
         env, _ = _env(n_agents=N, n_envs=B, episode_length=EL, seed=13)
