@@ -515,6 +515,11 @@ int eager_setup(gsm_handle *h) {
     const size_t words = std::max({2 * (size_t)nb, (size_t)nb + 2 * nc * kCsumStride,
                                    xw + (xw + gsm::kWave - 1) / gsm::kWave});
     const size_t bytes = 16 + words * sizeof(uint64_t);
+    if (h->eager_base) {   // (a retried setup)
+        (void)hipFree(h->eager_base);
+        h->eager_base = nullptr;
+        h->eager_gran = nullptr;
+    }
     e = gran_malloc(&h->eager_base, &h->eager_gran, bytes);
     h->eager_gran_end = h->eager_gran ? (uint64_t *)((char *)h->eager_gran + bytes) : nullptr;
     h->eager_csum = h->eager_gran ? h->eager_gran + 2 + nb : nullptr;
@@ -742,7 +747,9 @@ int gsm_bind(gsm_handle *h, const gsm_buffers *b) {
     p.lsa_stats = b->lsa_stats;
     h->bound = true;
     drop_graph(h);   // a captured graph holds the old pointers
-    if (h->eager_roll < 0) return eager_setup(h);
+    // (a failure here, e.g. no device yet, leaves the decision to the first
+    // step, which reports it)
+    if (h->eager_roll < 0 && eager_setup(h) != GSM_OK) h->eager_roll = -1;
     return GSM_OK;
 }
 
