@@ -208,7 +208,10 @@ int gsm_reset(gsm_handle *h, uint64_t seed, int reseed, const uint8_t *env_mask,
 
 /* Replaces env.step(action_n) (environment.py, SOURCES.txt:15): _set_action,
  * world.step() (core.py, SOURCES.txt:14), reward/cost/done callbacks and the
- * graph observation, for all B envs. actions: device pointer in action_fmt. */
+ * graph observation, for all B envs. actions: device pointer in action_fmt.
+ * One kernel launch (the config's rollout kernel with one step) at 6-24
+ * navigation agents, else a step kernel + an emit kernel; GSM_EAGER_ONE_LAUNCH
+ * (read at gsm_bind) forces either. Same outputs either way. */
 int gsm_step(gsm_handle *h, const void *actions, int action_fmt, void *stream);
 
 /* Recompute every output for the current state (after the caller rewrote
