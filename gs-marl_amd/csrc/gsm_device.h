@@ -455,19 +455,31 @@ __device__ __forceinline__ uint32_t pace_key() {
 }
 // the level from the CU counter as loaded after this workgroup's `done`-th
 // step was added to it
+// (diagnostic variants: -DGSM_PACE_T=t moves the thresholds to t/8 of a step,
+// -DGSM_PACE_LEVELS=4 adds a fourth level, behind by less than the threshold)
+#ifndef GSM_PACE_T
+#define GSM_PACE_T 4
+#endif
+#ifndef GSM_PACE_LEVELS
+#define GSM_PACE_LEVELS 3
+#endif
 __device__ __forceinline__ int pace_level(uint32_t fv, int done, int rank, int q) {
     const int arr = (int)(fv >> 24), tot = (int)(fv & (kPaceArrive - 1));
     // 8 x arrivals x (own steps - the CU's mean - (c - rank) x q / 4)
     const int x = 8 * (done * arr - tot) - arr * (arr - 1 - 2 * rank) * q;
-    return x >= 4 * arr ? 0 : x <= -4 * arr ? 2 : 1;
+    if constexpr (GSM_PACE_LEVELS == 4)
+        return x >= GSM_PACE_T * arr ? 0 : x >= 0 ? 1 : x > -GSM_PACE_T * arr ? 2 : 3;
+    return x >= GSM_PACE_T * arr ? 0 : x <= -GSM_PACE_T * arr ? 2 : 1;
 }
 __device__ __forceinline__ void pace_set(int lvl) {   // lvl wave-uniform
     if (lvl == 0)
         __builtin_amdgcn_s_setprio(0);
     else if (lvl == 1)
         __builtin_amdgcn_s_setprio(1);
-    else
+    else if (GSM_PACE_LEVELS == 3 || lvl == 2)
         __builtin_amdgcn_s_setprio(2);
+    else
+        __builtin_amdgcn_s_setprio(3);
 }
 
 // the priority of a rollout's first iterations, before the pace levels take
