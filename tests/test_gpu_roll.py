@@ -376,6 +376,50 @@ def test_roll_capture_refuses_action_rows_past_4gib():
     env.close()
 
 
+@pytest.mark.parametrize("N,B", [(24, 256), (12, 100)])
+def test_eager_captured_steps_between_one_launch_steps(N, B, monkeypatch):
+    """env.step inside a torch.cuda.graph capture takes the step + emit pair
+    (a captured rollout launch would replay one hand-off epoch); replays of
+    such a graph interleaved with the default one-launch eager steps leave
+    every buffer as the same sequence run with two launches everywhere
+    (GSM_EAGER_ONE_LAUNCH=0), auto-resets included."""
+    T, EL = 9, 4
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    got = []
+    for two in (True, False):
+        if two:
+            monkeypatch.setenv("GSM_EAGER_ONE_LAUNCH", "0")
+        else:
+            monkeypatch.delenv("GSM_EAGER_ONE_LAUNCH", raising=False)
+        env, _ = _env(n_agents=N, n_envs=B, episode_length=EL, seed=5)
+        env.reset(seed=5)
+        static = acts[0].clone()
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        s = torch.cuda.Stream(device=DEV)
+        with torch.cuda.stream(s):
+            with torch.cuda.graph(g, stream=s):
+                env.step(static, sync_edges=False)   # recorded, not run
+        torch.cuda.synchronize()
+        for t in range(T):
+            if t % 3 == 1:
+                static.copy_(acts[t])
+                g.replay()
+            else:
+                env.step(acts[t], sync_edges=False)
+        torch.cuda.synchronize()
+        assert not env.roll_gave_up()
+        got.append({k: v.clone() for k, v in env.t.items()})
+        del g
+        env.close()
+    ref = got[0]
+    for k in KEYS:
+        assert torch.equal(ref[k], got[1][k]), k
+    n = int(ref["edge_ptr"][-1])
+    assert torch.equal(ref["edge_index"][:, :n], got[1]["edge_index"][:, :n])
+    assert torch.equal(ref["edge_attr"][:n], got[1]["edge_attr"][:n])
+
+
 def test_roll_replay_refused_inside_stream_capture():
     """A rollout graph takes its own hand-off epoch and its half of the chunk-
     sum double buffer at every launch, so a launch recorded into the caller's
