@@ -570,20 +570,22 @@ def run_rank(args):
                 roll = False
         env.capture(actions, n, timing=False, slot=slot, kernels=gk)
 
-    settle = args.settle_ms > 0 and not eager and not stub and buf is None
+    settle = args.settle_ms > 0 and not stub and buf is None   # (eager / closed loop: EL eager steps per pass)
     if buf is not None:
         buf.reset(seed=cfg.seed)
         capture(EL, 0)
     elif not eager:
         if W > 0:
             capture(W, 2)
-        if settle:   # slot 3 holds a whole episode first, then the alignment
+        if settle:   # slot 3 holds a whole episode for the settle loop
             capture(EL, 3)
         elif A > 0:   # slot 3 is re-captured later by the roofline timing
             capture(A, 3)
         capture(chunk, 0)
         if rem:
             capture(rem, 1)
+        elif settle and A > 0:   # the alignment in slot 1, captured before the settle loop
+            capture(A, 1)
 
     obs = env.outputs()["obs"] if venv is not None else None
 
@@ -628,9 +630,25 @@ def run_rank(args):
         else:
             env.replay(slot)
 
+    # No collector pass inside the timed region (a full pass over torch's
+    # object graph takes milliseconds; it would land in one step's time), and
+    # none between the settle loop and the region either: milliseconds of an
+    # idle GPU there let its clocks drop, and the 2-3 ms after them ran the
+    # timed graphs slower — the h line 7.85 with the pass after the settle
+    # loop, 7.00 us/step without it, same box (profiles/r5_ab/bench_gc/). So
+    # everything that idles the GPU — the pass, the alignment's capture —
+    # comes first, then the settle loop, the warmup, the alignment and the
+    # region back to back.
+    metrics = torch.zeros(3, dtype=torch.float64, device=dev)
+    # ragged: the assignment warm start's certified / solved counters, read
+    # around the timed region (outside it)
+    lsa_stats = cfg.ragged and hasattr(env, "lsa_warm_stats")
+    gc.collect()
+    gc.disable()
     # settling (whole episodes: the alignment below still holds), warmup, then
     # the untimed alignment so the timed region holds an auto-reset
     settle_steps = 0
+    a_slot = 1 if (settle and A > 0 and not rem) else 3
     if settle:
         sync()
         t_s = time.perf_counter()
@@ -638,33 +656,28 @@ def run_rank(args):
             run_steps(EL, 3)
             settle_steps += EL
             sync()
-        if A > 0:
+        if A > 0 and a_slot == 3:   # (slot 1 holds the remainder graph)
             capture(A, 3)
-    # no collector pass inside the timed region (a full pass over torch's
-    # object graph takes milliseconds; it would land in one step's time) —
-    # collected before the warmup: milliseconds of an idle GPU right before
-    # the timed region let its clocks drop (the driver's 20-step line measured
-    # 12.4-12.7 us/step with the collection after the warmup, same box)
-    metrics = torch.zeros(3, dtype=torch.float64, device=dev)
-    # ragged: the assignment warm start's certified / solved counters, read
-    # around the timed region (outside it)
-    lsa_stats = cfg.ragged and hasattr(env, "lsa_warm_stats")
-    gc.collect()
-    gc.disable()
     for _ in range(W // EL if buf is not None else 0):
         run_steps(EL, 0)
     if W > 0 and buf is None:
         run_steps(W, 2)
     if A > 0:
-        run_steps(A, 3)
+        run_steps(A, a_slot)
     lsa0 = env.lsa_warm_stats() if lsa_stats else None
     sync()
     if world > 1:
         dist.barrier()
     sync()
+    # (diagnostic, GSM_BENCH_CHUNK_US=1: HIP events around every chunk of the
+    # timed region, device times to stderr; event packets in the region)
+    chunk_ev = ([torch.cuda.Event(enable_timing=True) for _ in range(n_chunks + 1)]
+                if os.environ.get("GSM_BENCH_CHUNK_US") and not stub else None)
     t0 = time.perf_counter()
     pending = None
-    for _ in range(n_chunks):
+    if chunk_ev:
+        chunk_ev[0].record()
+    for ci in range(n_chunks):
         if world > 1:
             # the only collective: the episode metrics as of this chunk's start,
             # SUM-reduced over RCCL/xGMI while the chunk's kernels run (the
@@ -674,6 +687,8 @@ def run_rank(args):
             metrics.copy_(env.episode_metrics())
             pending = all_reduce_metrics(metrics, async_op=True)
         run_steps(chunk, 0)
+        if chunk_ev:
+            chunk_ev[ci + 1].record()
     if rem:
         run_steps(rem, 1)
     if pending is not None:
@@ -682,6 +697,10 @@ def run_rank(args):
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    if chunk_ev:
+        log("timed region chunks (device us): " + ", ".join(
+            f"{chunk_ev[i].elapsed_time(chunk_ev[i + 1]) * 1e3:.1f}" for i in range(n_chunks))
+            + f"; wall {elapsed * 1e6:.1f}")
     gc.enable()
     lsa1 = env.lsa_warm_stats() if lsa0 is not None else None
 
