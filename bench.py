@@ -650,9 +650,25 @@ def run_rank(args):
     settle_steps = 0
     a_slot = 1 if (settle and A > 0 and not rem) else 3
     if settle:
+        # as many passes on every rank (the count for --settle-ms from the
+        # first pass, the max over ranks), started together: the ranks reach
+        # the region's barrier together instead of the early ones idling there
+        # (and their clocks dropping, as above) for the startup skew
+        sync()
+        if world > 1:
+            dist.barrier()
+        run_steps(EL, 3)   # (the first pass runs cold: the count from the second)
         sync()
         t_s = time.perf_counter()
-        while (time.perf_counter() - t_s) * 1e3 < args.settle_ms:
+        run_steps(EL, 3)
+        sync()
+        settle_steps += 2 * EL
+        passes = max(2, -(-int(args.settle_ms * 1e3) // max(1, int((time.perf_counter() - t_s) * 1e6))))
+        if world > 1:
+            pt = torch.tensor([passes], dtype=torch.int64, device=dev)
+            dist.all_reduce(pt, op=dist.ReduceOp.MAX)
+            passes = int(pt.item())
+        for _ in range(passes - 2):
             run_steps(EL, 3)
             settle_steps += EL
             sync()
