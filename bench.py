@@ -32,6 +32,7 @@ from __future__ import annotations
 import argparse
 import gc
 import json
+import math
 import os
 import sys
 import time
@@ -383,6 +384,10 @@ def parse_args(argv=None):
     ap.add_argument("--policy-graph", action="store_true",
                     help="the closed loop of --policy with the policy and env.step captured into one "
                          "torch.cuda graph per step (replayed every step)")
+    ap.add_argument("--vec-env", choices=("numpy-dense", "numpy-coo"), default=None,
+                    help="the MAPPO runner's host surface: GpuGraphVecEnv(output='numpy', graph=dense|coo)"
+                         ".step(host actions) per step, every returned array on the host (make_train_env's "
+                         "default is numpy-dense); context, not the headline")
     ap.add_argument("--unfused", action="store_true",
                     help="two launches per step in the graphs (no lagged emission)")
     ap.add_argument("--no-roll", action="store_true",
@@ -516,10 +521,17 @@ def run_rank(args):
     venv = None
     if args.policy_graph:
         args.policy = True
-    if args.policy and not stub:
-        # the vec-env a GS-MARL runner drives (gsmarl_amd/vec_env.py), on device
+    if args.vec_env and (args.policy or stub):
+        log("error: --vec-env drives the host surface with pre-generated actions (no --policy)")
+        return 2
+    if (args.policy or args.vec_env) and not stub:
+        # the vec-env a GS-MARL runner drives (gsmarl_amd/vec_env.py): on device
+        # (--policy), or its host arrays (--vec-env)
         from gsmarl_amd.vec_env import GpuGraphVecEnv
-        venv = GpuGraphVecEnv(cfg, dev, output="torch", graph="coo")
+        if args.vec_env:
+            venv = GpuGraphVecEnv(cfg, dev, output="numpy", graph=args.vec_env.split("-")[1])
+        else:
+            venv = GpuGraphVecEnv(cfg, dev, output="torch", graph="coo")
         env = venv.batch
     else:
         env = make_env(cfg, dev)
@@ -538,7 +550,7 @@ def run_rank(args):
     chunk = min(K, EL)
     n_chunks, rem = divmod(K, chunk)
     gk = "unfused" if args.unfused else "both"
-    eager = args.eager or args.policy
+    eager = args.eager or args.policy or bool(args.vec_env)
     roll = not (args.unfused or args.no_roll or eager or stub)
 
     buf = None
@@ -546,7 +558,7 @@ def run_rank(args):
         # the rollout buffer a runner fills: slot 0 = the episode's first
         # observation, step k into slot k + 1 (every step at distinct addresses)
         from gsmarl_amd import GraphRolloutBuffer
-        if args.eager or args.policy or args.no_roll or args.unfused:
+        if args.eager or args.policy or args.vec_env or args.no_roll or args.unfused:
             log("error: --buffer replays the buffer's captured episode (no --eager/--policy/--no-roll/--unfused)")
             return 2
         buf = GraphRolloutBuffer(env, episode_length=EL)
@@ -587,20 +599,27 @@ def run_rank(args):
         elif settle and A > 0:   # the alignment in slot 1, captured before the settle loop
             capture(A, 1)
 
-    obs = env.outputs()["obs"] if venv is not None else None
+    obs = env.outputs()["obs"] if venv is not None and not args.vec_env else None
+
+    # a trivial policy on device: the discrete action along the larger
+    # component of (target - position) (obs[..., 4:6]; actions 1/2 = +x/-x,
+    # 3/4 = +y/-y), as three kernels and no int64 scalar broadcasts: the
+    # goal's bearing, its quadrant sector (int32 directly) and the sector's
+    # action from a 5-entry table — the sectors in bearing order from -pi are
+    # W, S, E, N, W
+    sector_edges = torch.tensor([-0.75 * math.pi, -0.25 * math.pi, 0.25 * math.pi, 0.75 * math.pi],
+                                dtype=torch.float32, device=dev)
+    sector_action = torch.tensor([2, 4, 1, 3, 2], dtype=torch.int32, device=dev)
 
     def greedy(o):
-        """a trivial policy on device: the discrete action along the larger
-        component of (target - position) (obs[..., 4:6]; actions 1/2 = +x/-x,
-        3/4 = +y/-y)"""
-        dx, dy = o[..., 4], o[..., 5]
-        return torch.where(dx.abs() > dy.abs(), torch.where(dx > 0, 1, 2),
-                           torch.where(dy > 0, 3, 4)).to(torch.int32)
+        return sector_action[torch.bucketize(torch.atan2(o[..., 5], o[..., 4]), sector_edges, out_int32=True)]
 
     pgraph = None
     if args.policy_graph and not stub:
         # policy + env.step of one step as one torch CUDA graph (gsm_step on a
-        # capturing stream takes the two-launch path: no per-launch state)
+        # capturing stream records the one-launch step where the config has
+        # it: its hand-off epoch lives in device memory, so every replay
+        # takes a fresh one; else the step + emit pair)
         side = torch.cuda.Stream(device=dev)
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
@@ -611,11 +630,20 @@ def run_rank(args):
         with torch.cuda.graph(pgraph):
             venv.step(greedy(obs))   # obs: a view of the env's node features, static
 
+    host_actions = actions.cpu().numpy() if args.vec_env else None
+    vec_t = 0
+
     def run_steps(n, slot):
-        nonlocal obs
+        nonlocal obs, vec_t
         if pgraph is not None:
             for t in range(n):
                 pgraph.replay()
+        elif host_actions is not None:
+            # the runner's numpy loop: host actions in, host arrays and the
+            # lazy infos out (each call returns after its host copies)
+            for t in range(n):
+                venv.step(host_actions[vec_t % EL])
+                vec_t += 1
         elif venv is not None:
             for t in range(n):
                 obs = venv.step(greedy(obs))[0]
@@ -800,8 +828,13 @@ def run_rank(args):
                        "agents_per_step": agents,
                        "episode_length": EL, "mean_edges_per_env": round(total_edges / B, 2),
                        "parallelism": f"env-sharded x{world} (no data-path collective)",
-                       "launch": ("closed loop, one torch.cuda graph per step: greedy on-device policy(obs) + "
-                                  "GpuGraphVecEnv(output='torch', graph='coo').step (step + emit kernels)"
+                       "launch": (f"GpuGraphVecEnv(output='numpy', graph='{(args.vec_env or '-').split('-')[1]}')"
+                                  ".step(host int32 actions) per step: obs, agent_id, node_obs, adj as host arrays "
+                                  "(per-agent axes as broadcast views of one host copy per table), rewards, costs, "
+                                  "dones, LazyInfos" if args.vec_env else
+                                  "closed loop, one torch.cuda graph per step: greedy on-device policy(obs) + "
+                                  "GpuGraphVecEnv(output='torch', graph='coo').step (the one-launch step, device-side hand-off "
+                                  "epoch)"
                                   if pgraph is not None else
                                   "closed loop: GpuGraphVecEnv(output='torch', graph='coo').step(policy(obs)) "
                                   "per step, greedy on-device policy" if venv is not None else

@@ -78,6 +78,7 @@ struct gsm_handle {
     uint64_t *eager_csum = nullptr;           // its chunk-sum halves (segmented: inside eager_gran)
     int64_t eager_csum_half = 0;
     uint32_t eager_launches = 0;
+    uint32_t *eager_epoch = nullptr;  // the segmented one-launch step's device-side epoch (inside eager_gran)
     // gsm_step as a one-step rollout launch (step + its edges in one kernel):
     // -1 not yet decided for this config, 0 no (two launches), 1 yes
     int eager_roll = -1;
@@ -501,6 +502,8 @@ int eager_setup(gsm_handle *h) {
     const char *ev = getenv("GSM_EAGER_ONE_LAUNCH");
     const bool want = ev && *ev ? atoi(ev) != 0 : !tile && !gsm::roll_packed(p);
     if (!want) return GSM_OK;
+    const size_t nc = ((size_t)nb + gsm::kPrefixChunk - 1) / gsm::kPrefixChunk;
+    if (nc > (size_t)gsm::kWave) return GSM_OK;   // roll_prefix: one chunk sum per lane
     int dev = 0, per_cu = 0, n_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -511,10 +514,11 @@ int eager_setup(gsm_handle *h) {
     // segmented: aggregates + two halves of chunk sums; packed small envs:
     // per-wave counts + group sums)
     const size_t xw = (size_t)nb * gsm::kWavesPerBlock;
-    const size_t nc = ((size_t)nb + gsm::kPrefixChunk - 1) / gsm::kPrefixChunk;
     const size_t words = std::max({2 * (size_t)nb, (size_t)nb + 2 * nc * kCsumStride,
                                    xw + (xw + gsm::kWave - 1) / gsm::kWave});
-    const size_t bytes = 16 + words * sizeof(uint64_t);
+    // then the segmented step's device-side epoch replicas
+    const size_t epoch_bytes = (size_t)gsm::kEpochReps * gsm::kEpochStride * sizeof(uint32_t);
+    const size_t bytes = 16 + words * sizeof(uint64_t) + epoch_bytes;
     if (h->eager_base) {   // (a retried setup)
         (void)hipFree(h->eager_base);
         h->eager_base = nullptr;
@@ -524,9 +528,16 @@ int eager_setup(gsm_handle *h) {
     h->eager_gran_end = h->eager_gran ? (uint64_t *)((char *)h->eager_gran + bytes) : nullptr;
     h->eager_csum = h->eager_gran ? h->eager_gran + 2 + nb : nullptr;
     h->eager_csum_half = (int64_t)(nc * kCsumStride);
+    h->eager_epoch = h->eager_gran ? (uint32_t *)((char *)h->eager_gran + bytes - epoch_bytes) : nullptr;
     if (e != hipSuccess) { h->eager_gran = nullptr; return hip_fail(h, e, "hipMalloc (eager granules)"); }
     e = gsm::launch_granule_init(h->eager_gran, bytes, 0u, nullptr);
     if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
+    if (e == hipSuccess) {   // the first epoch: a fresh one of the process-wide sequence, in every replica
+        std::vector<uint32_t> ep((size_t)gsm::kEpochReps * gsm::kEpochStride, 0u);
+        const uint32_t e0 = next_launch_epoch();
+        for (int r = 0; r < gsm::kEpochReps; ++r) ep[(size_t)r * gsm::kEpochStride] = e0;
+        e = hipMemcpy(h->eager_epoch, ep.data(), epoch_bytes, hipMemcpyHostToDevice);
+    }
     if (e == hipSuccess && !h->roll_status) {
         e = hipMalloc(&h->roll_status, 16);
         if (e == hipSuccess) e = clear_status(h);
@@ -543,13 +554,20 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
         if (rc) return rc;
     }
     if (h->eager_roll == 0 || p.path == gsm::kPathRagged) return kEagerIneligible;
-    // a stream being captured into a graph (e.g. torch.cuda.graph around a
-    // policy + env.step): the two launches, which hold no per-launch state —
-    // a captured rollout launch would replay one launch epoch every time
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return kEagerIneligible;
     const bool tile = p.path == gsm::kPathTile;
-    const void *fn = tile ? gsm::roll_tile_kernel_fn(p, false) : gsm::roll_seg_kernel_fn(p, false);
+    // one env per wave: the kernel takes its epoch and chunk-sum half from
+    // device memory and advances them itself (gsm_roll_seg_kernel kEager), so
+    // the launch holds no per-launch host state and may be recorded into a
+    // stream capture (torch.cuda.graph around a policy + env.step). The tile
+    // and packed small-env forms take both from the host per launch: on a
+    // capturing stream they give way to the two launches, which hold none.
+    const void *fn = tile ? nullptr : gsm::roll_seg_eager_kernel_fn(p);
+    const bool dev_epoch = fn != nullptr;
+    if (!dev_epoch) {
+        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+        if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return kEagerIneligible;
+        fn = tile ? gsm::roll_tile_kernel_fn(p, false) : gsm::roll_seg_kernel_fn(p, false);
+    }
     if (!fn) return kEagerIneligible;   // (the action format may differ per call: checked every time)
     const int per_blk = tile ? 1 : gsm::roll_seg_envs_per_block(p);
     const int nb = tile ? gsm::step_grid_blocks(p) : (p.B + per_blk - 1) / per_blk;
@@ -560,15 +578,19 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
     const int xW = nb * gsm::kWavesPerBlock, xNG = (xW + gsm::kWave - 1) / gsm::kWave;
     // (one step: no pacing)
     p.roll = gsm::DevParams::Roll{(const char *)p.actions, 0, 1, 0, 1, xW, xNG, 0, 0, 0, h->eager_gran + 2,
-                                  h->roll_status, fresh_epoch(h->eager_last_epoch)};
-    const int par = (int)(h->eager_launches++ & 1u);
+                                  h->roll_status, dev_epoch ? 0u : fresh_epoch(h->eager_last_epoch)};
+    // (device epoch: the halves in a fixed order, the kernel picks by the
+    // epoch's parity; else this launch's half by the host's launch parity)
+    const int par = dev_epoch ? 0 : (int)(h->eager_launches & 1u);
     p.roll.csum = h->eager_csum + par * h->eager_csum_half;
     p.roll.csum_next = h->eager_csum + (1 - par) * h->eager_csum_half;
     p.roll.csum_stride = kCsumStride;
     p.roll.gran_end = h->eager_gran_end;
+    p.roll.dev_epoch = dev_epoch ? h->eager_epoch : nullptr;
     void *args[] = {&p};
     const hipError_t e = hipLaunchKernel(fn, dim3(nb), dim3(gsm::block_threads(p)), args, (unsigned)lds, s);
     if (e != hipSuccess) return hip_fail(h, e, "hipLaunchKernel (one-step rollout)");
+    ++h->eager_launches;   // (only a launched step takes a half: a failed one leaves the order as it was)
     return GSM_OK;
 }
 

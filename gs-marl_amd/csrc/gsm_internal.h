@@ -36,6 +36,10 @@ constexpr int kPaceKeys = 2048, kPaceStride = 16;   // counters, u32 words betwe
 // workgroups per chunk sum of the segmented rollout's one-hop CSR prefix
 // (gsm_device.h roll_prefix)
 constexpr int kPrefixChunk = 64;
+// the one-launch eager step's device-side epoch: replicas one per 64 bytes,
+// workgroup w reading replica w % kEpochReps (no single word read by the whole
+// grid at entry)
+constexpr int kEpochReps = 64, kEpochStride = 16;
 
 // Everything a launch needs, passed by value (kernarg segment, < 4 KB).
 // fp32 constants are formed on the host exactly as oracle/batch_ref.py:Spec
@@ -141,6 +145,9 @@ struct DevParams {
         // the checked build's address tests, gsm_device.h gran_chk)
         uint64_t *gran_end;
         int32_t *slab_end;
+        // the one-launch eager step's epoch in device memory (kEpochReps
+        // replicas kEpochStride u32 apart; gsm_roll_seg_kernel kEager)
+        uint32_t *dev_epoch;
     } roll;
     // A rollout's per-step outputs: step k's at base + k * stride (elements;
     // stride 0 = every step into the bound buffers, > 0 = a rollout buffer's
@@ -200,6 +207,8 @@ const void *emit_seg_kernel_fn(const DevParams &p);
 // fused K-step rollout kernel (nullptr where the config has none: G > 1,
 // runtime shapes, other families) and its LDS bytes
 const void *roll_seg_kernel_fn(const DevParams &p, bool slots);   // slots: a rollout buffer's outputs
+// the one-launch eager step (K = 1, device-side epoch; one env per wave shapes)
+const void *roll_seg_eager_kernel_fn(const DevParams &p);
 int roll_seg_envs_per_block(const DevParams &p);
 // the segmented rollout packs four small envs per wave (gsm_roll_pack_kernel):
 // per-wave CSR hand-off granules, as the ragged rollout (Roll::xW / xNG)

@@ -1198,10 +1198,19 @@ constexpr int roll_lds_force(int E) { return roll_lds_scr(E) + ((28 * E + 15) & 
 constexpr int roll_lds_wave(int N, int E) { return roll_lds_force(E) + 8 * N + 8 * kWave; }
 
 // kSlots: per-step outputs at base + k * stride (a rollout buffer); else every
-// step into the bound buffers (the strides are 0 and fold away)
-template <int kN, int kNo, int kFmt, bool kSlots>
+// step into the bound buffers (the strides are 0 and fold away).
+// kEager: the one-launch eager step (gsm_step, K = 1 at compile time). Its
+// hand-off epoch lives in device memory (p.roll.dev_epoch: kEpochReps
+// replicas), read by every workgroup at entry and advanced by the grid's last
+// workgroup once its final prefix is complete — by then every workgroup has
+// published its count, so has read the epoch — and the chunk-sum half is the
+// epoch's parity. No per-launch host state: a stream capture of env.step
+// (torch.cuda.graph around a policy and the step) records this launch and
+// every replay takes the next epoch.
+template <int kN, int kNo, int kFmt, bool kSlots, bool kEager = false>
 __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevParams p) {
     static_assert(kN > 0 && kN <= 31 && kNo <= 32 && kFmt >= 0, "compile-time shape, staged emission");
+    static_assert(!(kSlots && kEager), "the eager step writes the bound or redirected outputs");
     constexpr int N = kN, M = kN + kNo, E = 2 * kN + kNo;
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const Shape<kN, kNo> s(p);
@@ -1251,10 +1260,31 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     // rank-0 workgroup finish step 0 at 4.9 us and rank 7 at 21.5 us, and
     // iteration 2's emission waits for step 0 of every workgroup
     start_prio<3>();
+    // this launch's epoch (eager: from device memory, a replica per 64
+    // workgroups' neighbourhood; else a launch argument)
+    uint32_t epoch;
+    if constexpr (kEager)
+        epoch = __hip_atomic_load((gu32 *)(p.roll.dev_epoch + (blockIdx.x % kEpochReps) * kEpochStride),
+                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+        epoch = p.roll.epoch;
+    // the chunk sums of this launch and the half zeroed for the next one
+    // (eager: by the epoch's parity; else set per launch by the host)
+    auto csum_of = [&](KernargParams &q) -> uint64_t * {
+        if constexpr (kEager) return (epoch & 1u) ? q.roll.csum_next : q.roll.csum;
+        else return q.roll.csum;
+    };
+    auto csum_next_of = [&](KernargParams &q) -> uint64_t * {
+        if constexpr (kEager) return (epoch & 1u) ? q.roll.csum : q.roll.csum_next;
+        else return q.roll.csum_next;
+    };
     // pacing: this workgroup's CU counter (the arrival now, a step after each
     // step; its address re-formed at each use, no SGPRs held across the loop),
-    // and the counters of the slot's next launch zeroed
-    auto pacing = [] { return late_params().roll.pace != nullptr; };
+    // and the counters of the slot's next launch zeroed (none for one step)
+    auto pacing = [] {
+        if constexpr (kEager) return false;
+        else return late_params().roll.pace != nullptr;
+    };
     auto pace_ctr = [] { return (gu32 *)(late_params().roll.pace + pace_key()); };
     uint32_t pace_v = 0;   // thread 0: the arrivals before its own
     // one-hop prefix: chunks of 64 workgroups, their sums `cs` u64 apart; the
@@ -1262,9 +1292,10 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     const int nc = ((int)gridDim.x + kPrefixChunk - 1) / kPrefixChunk;
     {
         KernargParams &qz = late_params();
-        const int cs = qz.roll.csum_stride, n = qz.roll.K * nc;
+        const int cs = qz.roll.csum_stride, n = (kEager ? 1 : qz.roll.K) * nc;
+        uint64_t *const cz = csum_next_of(qz);
         for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
-            __hip_atomic_store((gu64 *)(qz.roll.csum_next + (int64_t)i * cs), 0ull, __ATOMIC_RELAXED,
+            __hip_atomic_store((gu64 *)(cz + (int64_t)i * cs), 0ull, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     }
     if (pacing()) {
@@ -1319,8 +1350,8 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         if (L0.agent) s_force[L0.m] = add_contacts(s_buf0, u, s_buf0[L0.m], cand_prev, late_params());
     }
 
-    const int K = p.roll.K, n_act = p.roll.n_actions;
-    const uint32_t etag = roll_epoch_tag(p.roll.epoch);     // this launch's tag base
+    const int K = kEager ? 1 : p.roll.K, n_act = p.roll.n_actions;
+    const uint32_t etag = roll_epoch_tag(epoch);            // this launch's tag base
     int arow = p.roll.t_first % n_act;                      // action row of the current step
     uint8_t deg = 0;                                        // App. A S16 flags of the final state
     // The edges of step t_first + j (j < K), emitted two iterations later
@@ -1343,8 +1374,16 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             KernargParams &qe = late_params();
             const uint32_t pv = done > 0 ? __hip_atomic_load(pace_ctr(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0u;
             const int cs = qe.roll.csum_stride;
-            const int ex = roll_prefix(qe.roll.gran + (int64_t)j * gridDim.x, qe.roll.csum + (int64_t)j * nc * cs, cs,
+            const int ex = roll_prefix(qe.roll.gran + (int64_t)j * gridDim.x, csum_of(qe) + (int64_t)j * nc * cs, cs,
                                        etag | (uint32_t)(j + 1), qe.roll.status, L.lane);
+            // eager: the grid's last workgroup, its prefix complete, has seen
+            // every other workgroup's count published — each read the epoch
+            // before — so the next launch's epoch goes out now
+            if constexpr (kEager) {
+                if (blockIdx.x == gridDim.x - 1 && L.lane < kEpochReps)
+                    __hip_atomic_store((gu32 *)(qe.roll.dev_epoch + L.lane * kEpochStride), (epoch + 1u) & 0xfffffu,
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
             // the pace level formed here once for the workgroup (wave-uniform
             // SALU work that every wave repeated before)
             const int lvl = done > 0 ? pace_level((uint32_t)__builtin_amdgcn_readfirstlane(pv), done,
@@ -1585,7 +1624,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
                 sum += s_bc[r3 * kWavesPerBlock + w];
             }
             const int cs = q.roll.csum_stride;
-            prefix_publish(q.roll.gran + (int64_t)k * gridDim.x, q.roll.csum + (int64_t)k * nc * cs, cs,
+            prefix_publish(q.roll.gran + (int64_t)k * gridDim.x, csum_of(q) + (int64_t)k * nc * cs, cs,
                            (int)blockIdx.x, etag | (uint32_t)(k + 1), (uint32_t)sum);
             // the last step's sums for the emit launch that follows, in the
             // config's workgroup layout: with G envs per wave the last of the
@@ -1668,8 +1707,18 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         asm volatile("" : "+v"(L.lane), "+v"(L.m));
         GSM_RSTAMP(p, L.b, 5);
         const int rm1 = r3 == 0 ? 2 : r3 - 1;   // (K - 1) % 3
-        if (K >= 2) emit_step(K - 2, rm1, rm1 == 0 ? 2 : rm1 - 1, s_row[L.lane], 0, L);
+        // Wave 0 hands each emission's offset over in s_red[0] before the
+        // emission's barrier. In the loop the publish barrier lies between
+        // two emissions; here they are adjacent, so a barrier first: no wave
+        // may still be about to read the previous emission's offset when
+        // wave 0 writes the next one (a wave held back by its priority would
+        // otherwise write step K - 2's edges at step K - 1's offset)
+        if (K >= 2) {
+            __syncthreads();
+            emit_step(K - 2, rm1, rm1 == 0 ? 2 : rm1 - 1, s_row[L.lane], 0, L);
+        }
         GSM_RSTAMP(p, L.b, 6);
+        __syncthreads();
         emit_step(K - 1, r3, rm1, oo, 0, L);
         GSM_RSTAMP(p, L.b, 7);
     }
@@ -2172,8 +2221,11 @@ bool roll_packed(const DevParams &p) {
 }
 int roll_seg_envs_per_block(const DevParams &p) { return roll_packed(p) ? kWavesPerBlock * kPackG : kWavesPerBlock; }
 
-template <bool kSlots>
+template <bool kSlots, bool kEager = false>
 static const void *pick_roll_seg(const DevParams &p) {
+    if constexpr (kEager) {   // (one env per wave only: the packed rollout keeps host epochs)
+        if (roll_packed(p)) return nullptr;
+    } else {
 #define GSM_PICK(n, no)                                                                            \
     if (p.N == n && p.No == no) {                                                                  \
         switch (p.action_fmt) {                                                                    \
@@ -2182,14 +2234,15 @@ static const void *pick_roll_seg(const DevParams &p) {
             default: return reinterpret_cast<const void *>(&gsm_roll_pack_kernel<n, no, 2, kSlots>); \
         }                                                                                          \
     }
-    GSM_PACK_SHAPES(GSM_PICK)
+        GSM_PACK_SHAPES(GSM_PICK)
 #undef GSM_PICK
+    }
 #define GSM_PICK(n, no)                                                                          \
     if (p.N == n && p.No == no) {                                                                \
         switch (p.action_fmt) {                                                                  \
-            case 0: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 0, kSlots>); \
-            case 1: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 1, kSlots>); \
-            default: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 2, kSlots>); \
+            case 0: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 0, kSlots, kEager>); \
+            case 1: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 1, kSlots, kEager>); \
+            default: return reinterpret_cast<const void *>(&gsm_roll_seg_kernel<n, no, 2, kSlots, kEager>); \
         }                                                                                        \
     }
     GSM_ROLL_SHAPES(GSM_PICK)
@@ -2199,6 +2252,10 @@ static const void *pick_roll_seg(const DevParams &p) {
 const void *roll_seg_kernel_fn(const DevParams &p, bool slots) {
     if (p.path != kPathSeg) return nullptr;
     return slots ? pick_roll_seg<true>(p) : pick_roll_seg<false>(p);
+}
+const void *roll_seg_eager_kernel_fn(const DevParams &p) {
+    if (p.path != kPathSeg) return nullptr;
+    return pick_roll_seg<false, true>(p);
 }
 size_t roll_kernel_lds(const DevParams &p) {
 #define GSM_PICK(n, no) \

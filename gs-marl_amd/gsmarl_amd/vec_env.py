@@ -4,7 +4,8 @@
 The reference (MAPPO / InforMARL lineage) runs ``n_rollout_threads`` env
 processes behind ``GraphSubprocVecEnv``: every step pickles actions down a pipe
 and observations back. Here all threads are one ``GpuBatchEnv`` on one GPU:
-``step`` is two kernel launches and nothing crosses a process boundary. The
+``step`` is one kernel launch (the one-launch step of the navigation shapes;
+the step + emit pair elsewhere) and nothing crosses a process boundary. The
 surface mirrors the ``ShareVecEnv`` API the runner calls — ``reset()``,
 ``step_async(actions)`` / ``step_wait()`` / ``step(actions)``, ``close()``,
 ``num_envs``, ``observation_space`` / ``share_observation_space`` /
@@ -24,13 +25,19 @@ the returned observation is the new episode's, as the MAPPO worker does.
 (InforMARL-style, gsmarl_amd.ego) instead of the shared absolute table.
 ``output="torch"`` keeps everything on the device (no host copies; node_obs /
 adj become expand() views, not copies); ``output="numpy"`` returns host arrays
-like the subprocess vec-env. ``graph="dense"`` builds the InforMARL dense
+like the subprocess vec-env — the per-env tables cross PCIe once and the
+per-agent axis is a read-only ``np.broadcast_to`` view of them (at 24 agents x
+8192 envs a materialised dense ``adj`` would be 4.1 GB per step, the view costs
+the 170 MB table), and ``infos`` is a lazy list (``LazyInfos``: the per-agent
+dicts are built when an env's entry is read). ``graph="dense"`` builds the InforMARL dense
 distance adjacency; ``graph="coo"`` returns ``adj=None`` and the batched COO
 graph is available from ``graph()`` (edge_index with global node ids,
 edge_attr distances, edge_ptr CSR offsets) — the form a PyG-style GNN consumes.
 """
 from __future__ import annotations
 
+import warnings
+from collections.abc import Sequence
 from typing import Optional
 
 import numpy as np
@@ -39,6 +46,50 @@ import torch
 from .batch import GpuBatchEnv
 from .config import EnvConfig
 from .spaces import Box, Discrete
+
+
+# host bytes per step above which output="numpy", graph="dense" warns at
+# construction (the [B, E, E] dense adjacency table that crosses PCIe)
+DENSE_HOST_WARN_BYTES = 256 << 20
+
+
+class LazyInfos(Sequence):
+    """The vec-env's ``infos``: a list of B per-env lists of N per-agent dicts
+    ({"cost"}, finished envs also {"episode": {"r", "c"}}, degenerate envs
+    {"degenerate"}), built when an env's entry is read instead of 196,608
+    dicts per step at the headline size. The step's costs, done flags,
+    degenerate flags and finished-episode totals come over in one host copy
+    each; ``finished`` (env indices) and ``episode_stats`` ([n, 2]: sum reward,
+    sum cost) give the finished episodes without building any dict."""
+
+    def __init__(self, cost: np.ndarray, done: np.ndarray, deg: np.ndarray, last: Optional[np.ndarray]):
+        self._cost, self._done, self._deg, self._last = cost, done, deg, last
+        self.finished = np.flatnonzero(done)
+        self.episode_stats = last[self.finished] if last is not None else np.zeros((0, 2), np.float32)
+
+    def __len__(self):
+        return self._cost.shape[0]
+
+    def _env(self, b):
+        row = [{"cost": float(c)} for c in self._cost[b]]
+        if self._deg[b]:   # App. A S16 flags (coincident colliders / non-finite agent)
+            for info in row:
+                info["degenerate"] = int(self._deg[b])
+        if self._done[b]:
+            ep = {"r": float(self._last[b, 0]), "c": float(self._last[b, 1])}
+            for info in row:
+                info["episode"] = dict(ep)
+        return row
+
+    def __getitem__(self, b):
+        if isinstance(b, slice):
+            return [self._env(i) for i in range(*b.indices(len(self)))]
+        b = int(b)
+        if b < 0:
+            b += len(self)
+        if not 0 <= b < len(self):
+            raise IndexError(b)
+        return self._env(b)
 
 
 class GpuGraphVecEnv:
@@ -71,6 +122,13 @@ class GpuGraphVecEnv:
         self._agent_id = torch.arange(N, device=self.batch.device, dtype=torch.int64).view(1, N, 1)
         # episode statistics of the envs that finished in the last step
         self.episode_returns = None
+        if output == "numpy" and graph == "dense":
+            B = cfg.n_envs
+            host = B * E * E * 4 + B * E * 7 * 4
+            if host > DENSE_HOST_WARN_BYTES:
+                warnings.warn(f"GpuGraphVecEnv(output='numpy', graph='dense') at {B} envs x {E} entities moves "
+                              f"{host / 2**20:.0f} MB to the host every step (the dense adjacency table); "
+                              "graph='coo' or output='torch' keep the graph on the device", stacklevel=2)
 
     # ------------------------------------------------------------- helpers
     def _actions(self, actions) -> torch.Tensor:
@@ -97,39 +155,36 @@ class GpuGraphVecEnv:
             return x
         return x.cpu().numpy()
 
+    def _per_agent(self, table):
+        """[B, ...] per-env table -> [B, N, ...] per agent: an expand() view on
+        the device, a read-only np.broadcast_to view of ONE host copy of the
+        table in numpy mode (the per-agent copies are never materialised)."""
+        B, N = self.num_envs, self.num_agents
+        if self.output == "torch":
+            return table.unsqueeze(1).expand(B, N, *table.shape[1:])
+        h = table.cpu().numpy()
+        return np.broadcast_to(h[:, None], (B, N) + h.shape[1:])
+
     def _graph_obs(self, out):
         B, N = self.num_envs, self.num_agents
         if self.node_obs == "ego":   # agent i's table relative to itself (gsmarl_amd.ego)
             from .ego import EgoView
-            node = EgoView(out["node_feat"], N).all()
+            node = self._host(EgoView(out["node_feat"], N).all())
         else:
-            node = out["node_feat"].unsqueeze(1).expand(B, N, *out["node_feat"].shape[1:])
-        adj = None
-        if self.graph_mode == "dense":
-            a = self._dense_adj(out)
-            adj = a.unsqueeze(1).expand(B, N, *a.shape[1:])
+            node = self._per_agent(out["node_feat"])
+        adj = self._per_agent(self._dense_adj(out)) if self.graph_mode == "dense" else None
         aid = self._agent_id.expand(B, N, 1)
-        return self._host(out["obs"]), self._host(aid), self._host(node), self._host(adj)
+        if self.output == "numpy":
+            aid = np.broadcast_to(np.arange(N, dtype=np.int64).reshape(1, N, 1), (B, N, 1))
+        return self._host(out["obs"]), aid, node, adj
 
     def _infos(self, out):
         """Per env, per agent dicts with the agent's cost; finished envs also
         carry the finished episode's totals (sum reward, sum cost), degenerate
-        envs their App. A S16 flags."""
-        c = out["cost"].cpu().numpy()
+        envs their App. A S16 flags — as a LazyInfos list."""
         d = out["done"].cpu().numpy().astype(bool)
-        deg = out["degenerate"].cpu().numpy()
         last = self.batch.t["ep_last"].cpu().numpy() if d.any() else None
-        infos = []
-        for b in range(self.num_envs):
-            row = [{"cost": float(c[b, i])} for i in range(self.num_agents)]
-            if deg[b]:   # App. A S16 flags (coincident colliders / non-finite agent)
-                for info in row:
-                    info["degenerate"] = int(deg[b])
-            if d[b]:
-                for info in row:
-                    info["episode"] = {"r": float(last[b, 0]), "c": float(last[b, 1])}
-            infos.append(row)
-        return infos
+        return LazyInfos(out["cost"].cpu().numpy(), d, out["degenerate"].cpu().numpy(), last)
 
     # ---------------------------------------------------------------- API
     def reset(self, seed: Optional[int] = None, env_mask=None):

@@ -378,8 +378,9 @@ def test_roll_capture_refuses_action_rows_past_4gib():
 
 @pytest.mark.parametrize("N,B", [(24, 256), (12, 100)])
 def test_eager_captured_steps_between_one_launch_steps(N, B, monkeypatch):
-    """env.step inside a torch.cuda.graph capture takes the step + emit pair
-    (a captured rollout launch would replay one hand-off epoch); replays of
+    """env.step inside a torch.cuda.graph capture records the one-launch step
+    (its hand-off epoch and chunk-sum half live in device memory and the
+    kernel advances them, so every replay takes a fresh epoch); replays of
     such a graph interleaved with the default one-launch eager steps leave
     every buffer as the same sequence run with two launches everywhere
     (GSM_EAGER_ONE_LAUNCH=0), auto-resets included."""
@@ -478,3 +479,60 @@ def test_roll_replay_after_its_stream_was_destroyed():
     assert not env.roll_gave_up()
     _same(ref, env, "roll across streams")
     env.close()
+
+
+def _greedy(o):
+    """the bench's closed-loop policy (int32 arithmetic): the discrete action
+    along the larger component of (goal - position)"""
+    dx, dy = o[..., 4], o[..., 5]
+    ax = 2 - (dx > 0).to(torch.int32)
+    ay = 4 - (dy > 0).to(torch.int32)
+    return torch.where(dx.abs() > dy.abs(), ax, ay)
+
+
+@pytest.mark.parametrize("N,B", [(24, 8192), (6, 300)])
+def test_captured_policy_step_replays(N, B, monkeypatch):
+    """The runner's captured step: one torch.cuda.graph holding the policy on
+    the current observation and env.step (the one-launch step, device-side
+    epoch) replayed back to back and interleaved with eager steps — three
+    replays in a row, then alternating — leaves every buffer, every step's
+    edges included, exactly as the same closed loop run with two launches per
+    step (GSM_EAGER_ONE_LAUNCH=0), auto-resets included."""
+    T, EL = 10, 4
+    pattern = "GGGEGEGGEG"   # G: graph replay, E: eager policy + step
+    got = []
+    for two in (True, False):
+        if two:
+            monkeypatch.setenv("GSM_EAGER_ONE_LAUNCH", "0")
+        else:
+            monkeypatch.delenv("GSM_EAGER_ONE_LAUNCH", raising=False)
+        env, _ = _env(n_agents=N, n_envs=B, episode_length=EL, seed=17)
+        env.reset(seed=17, sync_edges=False)
+        obs = env.t["node_feat"][:, :N, :6]
+        side = torch.cuda.Stream(device=DEV)
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            _greedy(obs)   # (warm the policy's kernels; no step)
+        torch.cuda.current_stream().wait_stream(side)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            env.step(_greedy(obs), sync_edges=False)   # recorded, not run
+        steps = []
+        for c in pattern[:T]:
+            if c == "G":
+                g.replay()
+            else:
+                env.step(_greedy(obs), sync_edges=False)
+            steps.append({k: env.t[k].clone() for k in ("edge_ptr", "reward", "cost", "done")} |
+                         {"edges": env.t["edge_index"][:, :int(env.t["edge_ptr"][-1])].clone()})
+        torch.cuda.synchronize()
+        assert not env.roll_gave_up()
+        got.append(({k: v.clone() for k, v in env.t.items()}, steps))
+        del g
+        env.close()
+    (ref, ref_steps), (one, one_steps) = got
+    for k in KEYS:
+        assert torch.equal(ref[k], one[k]), k
+    for t, (a, b) in enumerate(zip(ref_steps, one_steps)):
+        for k in a:
+            assert torch.equal(a[k], b[k]), (t, k)

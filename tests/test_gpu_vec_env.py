@@ -107,3 +107,47 @@ def test_ego_node_obs():
     for i in range(4):
         assert np.array_equal(node_n[i], EgoView(nf, 4)[i][0].cpu().numpy())
     env.close()
+
+
+def test_numpy_mode_broadcast_views_and_lazy_infos():
+    """output="numpy": node_obs / adj / agent_id are read-only broadcast views
+    of one host copy of each per-env table (no per-agent copies), equal to the
+    torch mode's expand() views; infos is a LazyInfos list whose entries and
+    finished-episode totals match the step's costs and ep_last."""
+    from gsmarl_amd import make_train_env
+    from gsmarl_amd.vec_env import LazyInfos
+    kw = dict(n_rollout_threads=64, num_agents=6, episode_length=3)
+    envs = make_train_env(_args(**kw), device=DEV)
+    tenv = make_train_env(_args(**kw), device=DEV, output="torch")
+    envs.reset(seed=5)
+    tenv.reset(seed=5)
+    acts = np.random.default_rng(1).integers(0, 5, size=(3, 64, 6)).astype(np.int32)
+    for t in range(3):
+        obs, aid, node, adj, rew, cost, done, infos = envs.step(acts[t])
+        tob, taid, tnode, tadj, *_ = tenv.step(acts[t])
+    assert node.strides[1] == 0 and adj.strides[1] == 0 and aid.strides[0] == 0
+    assert not node.flags.writeable
+    assert np.array_equal(node, tnode.cpu().numpy()) and np.array_equal(adj, tadj.cpu().numpy())
+    assert np.array_equal(aid, taid.cpu().numpy()) and np.array_equal(obs, tob.cpu().numpy())
+    assert isinstance(infos, LazyInfos) and len(infos) == 64
+    assert np.array_equal(infos.finished, np.arange(64))          # episode_length 3: all finished
+    last = envs.batch.t["ep_last"].cpu().numpy()
+    assert np.array_equal(infos.episode_stats, last)
+    assert infos[5][2]["cost"] == float(cost[5, 2, 0])
+    assert infos[-1][0]["episode"] == {"r": float(last[63, 0]), "c": float(last[63, 1])}
+    assert len(infos[10:13]) == 3 and len(list(iter(infos))) == 64
+    envs.close()
+    tenv.close()
+
+
+def test_dense_numpy_mode_warns_at_headline_size():
+    """output="numpy", graph="dense" past 256 MB of host tables per step warns
+    at construction (24 agents x 8192 envs: 170 MB of adjacency + 16 MB of node
+    features per step stays under it; 96 agents x 1024 envs: 340 MB warns)."""
+    import warnings as w
+    from gsmarl_amd import EnvConfig, GpuGraphVecEnv
+    with w.catch_warnings():
+        w.simplefilter("error")
+        GpuGraphVecEnv(EnvConfig(n_agents=24, n_envs=8192), DEV).close()
+    with pytest.warns(UserWarning, match="graph='coo'"):
+        GpuGraphVecEnv(EnvConfig(n_agents=96, n_envs=1024), DEV).close()
