@@ -384,6 +384,10 @@ def parse_args(argv=None):
     ap.add_argument("--policy-graph", action="store_true",
                     help="the closed loop of --policy with the policy and env.step captured into one "
                          "torch.cuda graph per step (replayed every step)")
+    ap.add_argument("--policy-act", choices=("index", "cont"), default="index",
+                    help="--policy / --policy-graph action format: index = the greedy discrete action (int32, "
+                         "three small kernels), cont = the continuous bang-bang action sign(goal - position) "
+                         "(one kernel)")
     ap.add_argument("--vec-env", choices=("numpy-dense", "numpy-coo"), default=None,
                     help="the MAPPO runner's host surface: GpuGraphVecEnv(output='numpy', graph=dense|coo)"
                          ".step(host actions) per step, every returned array on the host (make_train_env's "
@@ -612,6 +616,8 @@ def run_rank(args):
     sector_action = torch.tensor([2, 4, 1, 3, 2], dtype=torch.int32, device=dev)
 
     def greedy(o):
+        if args.policy_act == "cont":   # MPE continuous actions, u = a * sensitivity: one kernel
+            return torch.sign(o[..., 4:6])
         return sector_action[torch.bucketize(torch.atan2(o[..., 5], o[..., 4]), sector_edges, out_int32=True)]
 
     pgraph = None
@@ -832,7 +838,8 @@ def run_rank(args):
                                   ".step(host int32 actions) per step: obs, agent_id, node_obs, adj as host arrays "
                                   "(per-agent axes as broadcast views of one host copy per table), rewards, costs, "
                                   "dones, LazyInfos" if args.vec_env else
-                                  "closed loop, one torch.cuda graph per step: greedy on-device policy(obs) + "
+                                  f"closed loop, one torch.cuda graph per step: greedy on-device policy(obs) "
+                                  f"({'continuous sign(goal - pos), one kernel' if args.policy_act == 'cont' else 'discrete, three kernels'}) + "
                                   "GpuGraphVecEnv(output='torch', graph='coo').step (the one-launch step, device-side hand-off "
                                   "epoch)"
                                   if pgraph is not None else

@@ -79,6 +79,7 @@ struct gsm_handle {
     int64_t eager_csum_half = 0;
     uint32_t eager_launches = 0;
     uint32_t *eager_epoch = nullptr;  // the segmented one-launch step's device-side epoch (inside eager_gran)
+    bool eager_dev_epoch = true;      // GSM_EAGER_DEV_EPOCH=0 (an A/B knob): host epochs outside captures
     // gsm_step as a one-step rollout launch (step + its edges in one kernel):
     // -1 not yet decided for this config, 0 no (two launches), 1 yes
     int eager_roll = -1;
@@ -504,6 +505,8 @@ int eager_setup(gsm_handle *h) {
     if (!want) return GSM_OK;
     const size_t nc = ((size_t)nb + gsm::kPrefixChunk - 1) / gsm::kPrefixChunk;
     if (nc > (size_t)gsm::kWave) return GSM_OK;   // roll_prefix: one chunk sum per lane
+    const char *de = getenv("GSM_EAGER_DEV_EPOCH");
+    h->eager_dev_epoch = !(de && *de && atoi(de) == 0);
     int dev = 0, per_cu = 0, n_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
@@ -562,10 +565,12 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
     // and packed small-env forms take both from the host per launch: on a
     // capturing stream they give way to the two launches, which hold none.
     const void *fn = tile ? nullptr : gsm::roll_seg_eager_kernel_fn(p);
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    const bool capturing = hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone;
+    if (fn && !capturing && !h->eager_dev_epoch) fn = nullptr;
     const bool dev_epoch = fn != nullptr;
     if (!dev_epoch) {
-        hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-        if (hipStreamIsCapturing(s, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return kEagerIneligible;
+        if (capturing) return kEagerIneligible;
         fn = tile ? gsm::roll_tile_kernel_fn(p, false) : gsm::roll_seg_kernel_fn(p, false);
     }
     if (!fn) return kEagerIneligible;   // (the action format may differ per call: checked every time)

@@ -1264,8 +1264,9 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     // workgroups' neighbourhood; else a launch argument)
     uint32_t epoch;
     if constexpr (kEager)
-        epoch = __hip_atomic_load((gu32 *)(p.roll.dev_epoch + (blockIdx.x % kEpochReps) * kEpochStride),
-                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        epoch = __builtin_amdgcn_readfirstlane(__hip_atomic_load(
+            (gu32 *)(p.roll.dev_epoch + (blockIdx.x % kEpochReps) * kEpochStride), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT));
     else
         epoch = p.roll.epoch;
     // the chunk sums of this launch and the half zeroed for the next one
@@ -1290,14 +1291,17 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     // one-hop prefix: chunks of 64 workgroups, their sums `cs` u64 apart; the
     // slot's next launch's chunk sums zeroed
     const int nc = ((int)gridDim.x + kPrefixChunk - 1) / kPrefixChunk;
-    {
+    auto zero_next_csums = [&] {
         KernargParams &qz = late_params();
         const int cs = qz.roll.csum_stride, n = (kEager ? 1 : qz.roll.K) * nc;
         uint64_t *const cz = csum_next_of(qz);
         for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
             __hip_atomic_store((gu64 *)(cz + (int64_t)i * cs), 0ull, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
-    }
+    };
+    // (eager: behind the state loads, so that they need not wait for the
+    // epoch load that picks the half)
+    if constexpr (!kEager) zero_next_csums();
     if (pacing()) {
         KernargParams &qz = late_params();
         for (int i = blockIdx.x * kBlock + threadIdx.x; i < kPaceKeys; i += gridDim.x * kBlock)
@@ -1310,6 +1314,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     // ---- the state before step t_first and step t_first's actions
     // (p.actions); the edges of that state were emitted by whatever ran before
     SegIn in = seg_load<kN, kNo, kFmt, true>(p, s, L0);
+    if constexpr (kEager) zero_next_csums();   // (the state loads in flight: only the epoch is waited for)
     seg_load_finish<kN, kNo, kFmt, true>(p, L0, in);
     int t = in.t, ep = in.ep;
     float2 acc = in.acc, v = in.v, u = in.u;

@@ -206,7 +206,8 @@ class GpuGraphVecEnv:
         obs, aid, node, adj = self._graph_obs(out)
         rew = out["reward"].unsqueeze(-1)
         cost = out["cost"].unsqueeze(-1)
-        done = out["done"].bool().unsqueeze(1).expand(self.num_envs, self.num_agents)
+        # (u8 0/1 reinterpreted as bool: a view, no conversion kernel)
+        done = out["done"].view(torch.bool).unsqueeze(1).expand(self.num_envs, self.num_agents)
         infos = self._infos(out) if self.output == "numpy" else None
         return obs, aid, node, adj, self._host(rew), self._host(cost), self._host(done), infos
 
