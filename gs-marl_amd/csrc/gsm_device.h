@@ -261,8 +261,22 @@ __device__ __forceinline__ const uint64_t *gran_chk(const uint64_t *g) {
     }
     return g;
 }
+// any other hand-off word of the slot's allocation (chunk sums, pacing
+// counters, the eager step's epoch replicas): the same test
+template <typename T>
+__device__ __forceinline__ T *hand_chk(T *g) {
+    KernargParams &q = late_params();
+    const char *c = (const char *)g;
+    if (__builtin_expect(c < (const char *)q.roll.gran || c + sizeof(T) > (const char *)q.roll.gran_end, 0)) {
+        __hip_atomic_store((gu32 *)q.roll.status, kStatusOutOfBounds, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return (T *)q.roll.gran;
+    }
+    return g;
+}
 #else
 __device__ __forceinline__ const uint64_t *gran_chk(const uint64_t *g) { return g; }
+template <typename T>
+__device__ __forceinline__ T *hand_chk(T *g) { return g; }
 #endif
 __device__ __forceinline__ uint64_t gran_ld(const uint64_t *g) {
     return __hip_atomic_load((const gu64 *)gran_chk(g), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -512,7 +526,7 @@ __device__ __forceinline__ void start_prio() {
 __device__ __forceinline__ void prefix_publish(uint64_t *agg_s, uint64_t *sum_s, int cs, int w, uint32_t tag,
                                                uint32_t v) {
     gran_st(agg_s + w, (uint64_t)tag << 32 | v);
-    (void)__hip_atomic_fetch_add((gu64 *)(sum_s + (int64_t)(w / kPrefixChunk) * cs), 1ull << 32 | v,
+    (void)__hip_atomic_fetch_add((gu64 *)hand_chk(sum_s + (int64_t)(w / kPrefixChunk) * cs), 1ull << 32 | v,
                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 // Workgroup w's exclusive prefix of step s (ONE wave; wave-uniform result).
@@ -525,7 +539,7 @@ __device__ __forceinline__ int roll_prefix(const uint64_t *agg_s, const uint64_t
     int w = (int)blockIdx.x;
     asm volatile("" : "+s"(w));   // no window predicates hoisted into a rollout's loop (SGPR pairs)
     const int c = w / kPrefixChunk, r = w % kPrefixChunk;
-    const uint64_t *sp = sum_s + (int64_t)min(lane, c > 0 ? c - 1 : 0) * cs;
+    const uint64_t *sp = hand_chk(sum_s + (int64_t)min(lane, c > 0 ? c - 1 : 0) * cs);
     const uint64_t *ap = agg_s + c * kPrefixChunk + min(lane, r > 0 ? r - 1 : 0);
     uint64_t sv = __hip_atomic_load((const gu64 *)sp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     uint64_t av = gran_ld(ap);

@@ -335,6 +335,9 @@ __device__ __forceinline__ LsaLds lsa_lds(unsigned char *lds, int nmax) {
 // loop's chain, same values: identical results).
 // s_agent: the agents' positions in LDS (rows 0..N-1: the staged storage
 // rows), read as broadcasts when the cost matrix is built
+#ifndef GSM_LSA_ROLL_CHUNK
+#define GSM_LSA_ROLL_CHUNK 4
+#endif
 template <bool kColLds = false>
 __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const float2 *s_agent, const LsaLds &sl, float *own,
                         LsaWarm w, int *iters = nullptr, uint64_t *tm = nullptr) {
@@ -380,6 +383,11 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const float2 *s
         }
     }
     const int ccl = col ? lane : 0;   // kColLds: this lane's column (lanes past N read column 0, never used)
+    // LDS operands per wait in the warm start's row / column passes: 8, or 4
+    // in the rollout (kColLds), whose 64-VGPR budget spilled the 8-wide chunk's
+    // 24 registers to scratch inside the step loop — private lines of every
+    // wave, evicted from L2 to HBM
+    constexpr int kPassChunk = kColLds ? GSM_LSA_ROLL_CHUNK : 8;
     wave_sync();
     LSA_T(0);
     const double kInf = __builtin_inf();
@@ -594,16 +602,16 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const float2 *s
                     // N hold +inf (and v = 0): r = +inf, no per-column test
                     // (the minimum by v_min_f64: no zero of either sign
                     // arises, C - v is +0 when equal, and no NaN)
-                    for (int j0 = 0; j0 < n8; j0 += 8) {
-                        float cr[8];
-                        double vj[8];
+                    for (int j0 = 0; j0 < n8; j0 += kPassChunk) {
+                        float cr[kPassChunk];
+                        double vj[kPassChunk];
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) {
+                        for (int k = 0; k < kPassChunk; ++k) {
                             cr[k] = crow[j0 + k];
                             vj[k] = sl.v[j0 + k];
                         }
 #pragma unroll
-                        for (int k = 0; k < 8; ++k) m = fmin(m, (double)cr[k] - vj[k]);
+                        for (int k = 0; k < kPassChunk; ++k) m = fmin(m, (double)cr[k] - vj[k]);
                     }
                     // the previous column's reduced cost, the same expression as in the scan
                     rc = (c0 >= 0 && c0 < N) ? (double)crow[c0] - sl.v[c0] : kInf;
@@ -621,16 +629,16 @@ __device__ int wave_lsa(int N, int lane, float2 pa, float2 slot, const float2 *s
             wave_sync();
             if (col) {
                 double cm = kInf;
-                for (int i0 = 0; i0 < n8; i0 += 8) {   // chunks of 8 rows, reads first
-                    float cc[8];
-                    double ui[8];
+                for (int i0 = 0; i0 < n8; i0 += kPassChunk) {   // chunks of rows, reads first
+                    float cc[kPassChunk];
+                    double ui[kPassChunk];
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) {
+                    for (int k = 0; k < kPassChunk; ++k) {
                         cc[k] = s_cost[(i0 + k) * S + lane];
                         ui[k] = sl.u[i0 + k];
                     }
 #pragma unroll
-                    for (int k = 0; k < 8; ++k) cm = fmin(cm, (double)cc[k] - ui[k]);
+                    for (int k = 0; k < kPassChunk; ++k) cm = fmin(cm, (double)cc[k] - ui[k]);
                 }
                 v = cm;
             }

@@ -1265,7 +1265,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     uint32_t epoch;
     if constexpr (kEager)
         epoch = __builtin_amdgcn_readfirstlane(__hip_atomic_load(
-            (gu32 *)(p.roll.dev_epoch + (blockIdx.x % kEpochReps) * kEpochStride), __ATOMIC_RELAXED,
+            (gu32 *)hand_chk(p.roll.dev_epoch + (blockIdx.x % kEpochReps) * kEpochStride), __ATOMIC_RELAXED,
             __HIP_MEMORY_SCOPE_AGENT));
     else
         epoch = p.roll.epoch;
@@ -1286,7 +1286,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         if constexpr (kEager) return false;
         else return late_params().roll.pace != nullptr;
     };
-    auto pace_ctr = [] { return (gu32 *)(late_params().roll.pace + pace_key()); };
+    auto pace_ctr = [] { return (gu32 *)hand_chk(late_params().roll.pace + pace_key()); };
     uint32_t pace_v = 0;   // thread 0: the arrivals before its own
     // one-hop prefix: chunks of 64 workgroups, their sums `cs` u64 apart; the
     // slot's next launch's chunk sums zeroed
@@ -1296,7 +1296,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
         const int cs = qz.roll.csum_stride, n = (kEager ? 1 : qz.roll.K) * nc;
         uint64_t *const cz = csum_next_of(qz);
         for (int i = blockIdx.x * kBlock + threadIdx.x; i < n; i += gridDim.x * kBlock)
-            __hip_atomic_store((gu64 *)(cz + (int64_t)i * cs), 0ull, __ATOMIC_RELAXED,
+            __hip_atomic_store((gu64 *)hand_chk(cz + (int64_t)i * cs), 0ull, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     };
     // (eager: behind the state loads, so that they need not wait for the
@@ -1305,7 +1305,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     if (pacing()) {
         KernargParams &qz = late_params();
         for (int i = blockIdx.x * kBlock + threadIdx.x; i < kPaceKeys; i += gridDim.x * kBlock)
-            __hip_atomic_store((gu32 *)(qz.roll.pace_next + i * kPaceStride), 0u, __ATOMIC_RELAXED,
+            __hip_atomic_store((gu32 *)hand_chk(qz.roll.pace_next + i * kPaceStride), 0u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         if (threadIdx.x == 0)
             pace_v = __hip_atomic_fetch_add(pace_ctr(), kPaceArrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1386,7 +1386,7 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
             // before — so the next launch's epoch goes out now
             if constexpr (kEager) {
                 if (blockIdx.x == gridDim.x - 1 && L.lane < kEpochReps)
-                    __hip_atomic_store((gu32 *)(qe.roll.dev_epoch + L.lane * kEpochStride), (epoch + 1u) & 0xfffffu,
+                    __hip_atomic_store((gu32 *)hand_chk(qe.roll.dev_epoch + L.lane * kEpochStride), (epoch + 1u) & 0xfffffu,
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             // the pace level formed here once for the workgroup (wave-uniform
@@ -1693,8 +1693,12 @@ __global__ __launch_bounds__(kBlock) GSM_ROLL_ATTR void gsm_roll_seg_kernel(DevP
     if (wave_live) {
         float2 *const pos_b = q.pos + eb * E;
         const float2 *const s_pos = pos_buf(r3);
-        if (L0.lane < E) pos_b[L0.lane] = s_pos[L0.lane];
-        if (L0.lane + kWave < E) pos_b[L0.lane + kWave] = s_pos[L0.lane + kWave];
+        // (eager: the goal / obstacle rows change only with a re-layout — for
+        // K = 1 the last iteration's, relaid_prev — so otherwise the agents'
+        // rows only: 384 of 576 bytes per env less at 24 agents)
+        const int n_rows = (kEager && !relaid_prev) ? N : E;
+        if (L0.lane < n_rows) pos_b[L0.lane] = s_pos[L0.lane];
+        if (L0.lane + kWave < n_rows) pos_b[L0.lane + kWave] = s_pos[L0.lane + kWave];
         if (L0.agent) {
             (q.vel + eb * N)[L0.lane] = v;
             (q.contact_mask + eb * N)[L0.lane] = cand_prev;

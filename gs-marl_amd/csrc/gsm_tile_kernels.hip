@@ -832,7 +832,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     // arrival now, a step after each step, its rank = the arrivals before it;
     // the address re-formed at each use), the slot's next counters zeroed
     auto pacing = [] { return late_params().roll.pace != nullptr; };
-    auto pace_ctr = [] { return (gu32 *)(late_params().roll.pace + pace_key()); };
+    auto pace_ctr = [] { return (gu32 *)hand_chk(late_params().roll.pace + pace_key()); };
     // the one-hop CSR prefix (gsm_device.h roll_prefix): chunks of 64
     // workgroups; the slot's next launch's chunk sums zeroed
     const int nc = ((int)gridDim.x + kPrefixChunk - 1) / kPrefixChunk;
@@ -840,13 +840,13 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         KernargParams &qz = late_params();
         const int cs = qz.roll.csum_stride, n = qz.roll.K * nc;
         for (int i = b * kTileBlock + tid; i < n; i += gridDim.x * kTileBlock)
-            __hip_atomic_store((gu64 *)(qz.roll.csum_next + (int64_t)i * cs), 0ull, __ATOMIC_RELAXED,
+            __hip_atomic_store((gu64 *)hand_chk(qz.roll.csum_next + (int64_t)i * cs), 0ull, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
     }
     if (pacing()) {
         KernargParams &qz = late_params();
         for (int i = b * kTileBlock + tid; i < kPaceKeys; i += gridDim.x * kTileBlock)
-            __hip_atomic_store((gu32 *)(qz.roll.pace_next + i * kPaceStride), 0u, __ATOMIC_RELAXED,
+            __hip_atomic_store((gu32 *)hand_chk(qz.roll.pace_next + i * kPaceStride), 0u, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         if (tid == 0)
             s_x[3] = (int)(__hip_atomic_fetch_add(pace_ctr(), kPaceArrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >>

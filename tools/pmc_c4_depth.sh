@@ -1,7 +1,11 @@
+# C4 ragged rollout: PMC HBM traffic per step (FETCH_SIZE x2 + WRITE_SIZE, the
+# gfx950 correction of MI355X_MICROARCH.md) at each edge-slab depth
+# (GSM_ROLL_DEPTH). Usage: bash tools/pmc_c4_depth.sh TAG depth ...
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"; export TMPDIR=/tmp
-O=$GRAFT_REPO_ROOT/gpurun_out/r5v; mkdir -p $O
-for d in 2 4 8; do
+T=$1; shift
+O=$GRAFT_REPO_ROOT/gpurun_out/$T; mkdir -p $O
+for d in "${@:-2 4 8}"; do
   for c in FETCH_SIZE WRITE_SIZE; do
     ( cd /tmp && GSM_ROLL_DEPTH=$d timeout -s KILL 240 rocprofv3 --pmc $c --output-format csv -d $O/d${d}_$c -o run -- python3 $GRAFT_REPO_ROOT/bench.py --config c4 --no-cpu-baseline --no-kernel-timing --settle-ms 0 --warmup 0 --no-align --steps 100 > $O/d${d}_$c.log 2>&1 ) || { echo "fail d=$d $c"; tail -5 $O/d${d}_$c.log; exit 1; }
     python3 - $O/d${d}_$c $c $d <<'PY'
