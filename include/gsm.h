@@ -284,10 +284,15 @@ int gsm_observe_into(gsm_handle *h, const gsm_outputs *out, void *stream);
  * capacity, allocated on first use, since a workgroup may trail its
  * successors by steps). Combines with GSM_GRAPH_TIME_ENDS only (the events
  * then bracket the launch: gsm_graph_kernel_ms gives its time per step);
- * GSM_EINVAL where the config has no rollout kernel, or where the action rows
+ * GSM_EINVAL where the config has no rollout kernel, where the action rows
  * span 4 GiB or more (n_actions * action_stride_bytes >= 2^32: the rollout
- * kernels address them with 32-bit offsets; without GSM_GRAPH_ROLL such a
- * capture takes the per-step chain). */
+ * kernels address them with 32-bit offsets), where n_steps > 4094, or where
+ * the batch exceeds one residency round of the rollout kernel (occupancy x
+ * CUs; on an MI355X 8192 envs of the one-env-per-wave and ragged rollouts —
+ * 2048 workgroups, also the bound of the one-hop CSR prefix's 64 chunk sums of
+ * 64 workgroups — 16384 of the packed small-env rollout, 1024 of the tile
+ * rollout; shard larger batches across handles or GPUs, env_base). Without
+ * GSM_GRAPH_ROLL such a capture takes the per-step chain instead. */
 #define GSM_GRAPH_ROLL 64
 int gsm_graph_capture(gsm_handle *h, int32_t slot, const void *actions, int64_t action_stride_bytes,
                       int32_t n_actions, int32_t n_steps, int action_fmt, int flags);

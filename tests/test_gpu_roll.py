@@ -536,3 +536,31 @@ def test_captured_policy_step_replays(N, B, monkeypatch):
     for t, (a, b) in enumerate(zip(ref_steps, one_steps)):
         for k in a:
             assert torch.equal(a[k], b[k]), (t, k)
+
+
+@pytest.mark.parametrize("N,B", [(24, 8193), (96, 1025)])
+def test_roll_capture_refuses_past_one_residency_round(N, B):
+    """A batch past one residency round of its rollout kernel (8192 envs of
+    the one-env-per-wave rollout: 2048 workgroups, the one-hop prefix's 64 x
+    64; 1024 of the tile rollout) is refused by an explicit GSM_GRAPH_ROLL
+    capture (GSM_EINVAL, gsm.h) before anything launches; the default capture
+    takes the per-step chain, which equals eager steps."""
+    import ctypes as C
+
+    from gsmarl_amd import _lib
+    T = 3
+    env, _ = _env(n_agents=N, n_envs=B, episode_length=2)
+    acts = torch.randint(0, 5, (T, B, N), dtype=torch.int32, device=DEV)
+    ptr = C.c_void_p(acts.data_ptr())
+    stride = acts[0].numel() * 4
+    rc = env.lib.gsm_graph_capture(env._h, 0, ptr, stride, T, T, _lib.ACT_INDEX, _lib.GRAPH_ROLL)
+    assert rc == _lib.GSM_EINVAL
+    assert "residency round" in _lib.last_error(env.lib, env._h)
+    ref = _eager(env, acts, T, seed=6)
+    env.reset(seed=6)
+    env.capture(acts, T, slot=0, kernels="both")
+    assert not env.graph_is_rollout(0)
+    env.replay(0)
+    torch.cuda.synchronize()
+    _same(ref, env, "chain past one residency round")
+    env.close()
