@@ -84,8 +84,8 @@ pmc_key() {   # the profiles/pmc_kernels.json key spec of a collected configurat
 
 case $CMD in
   tests)
-    K=${1:+-k "$1"}
-    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider $K > $O/pytest_gpu.log 2>&1; rc=$?
+    K=(); [ -n "$1" ] && K=(-k "$1")
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread -p no:cacheprovider "${K[@]}" > $O/pytest_gpu.log 2>&1; rc=$?
     grep -E "passed|failed|error" $O/pytest_gpu.log | tail -3
     [ $rc -eq 0 ] || { grep -B5 -A40 "FAILED\|Error" $O/pytest_gpu.log | head -80; exit $rc; }
     grep "max |" $O/pytest_gpu.log | sort -k2 | tail -2
