@@ -510,7 +510,7 @@ int eager_setup(gsm_handle *h) {
     int dev = 0, per_cu = 0, n_cu = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, gsm::block_threads(p), lds);
+    if (e == hipSuccess) e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, gsm::roll_block_threads(p), lds);
     if (e != hipSuccess) return hip_fail(h, e, "occupancy query (eager rollout)");
     if ((int64_t)per_cu * n_cu < nb) return GSM_OK;
     // (tile path: aggregates + inclusive prefixes per workgroup;
@@ -593,7 +593,7 @@ int launch_step_roll(gsm_handle *h, gsm::DevParams p, hipStream_t s) {
     p.roll.gran_end = h->eager_gran_end;
     p.roll.dev_epoch = dev_epoch ? h->eager_epoch : nullptr;
     void *args[] = {&p};
-    const hipError_t e = hipLaunchKernel(fn, dim3(nb), dim3(gsm::block_threads(p)), args, (unsigned)lds, s);
+    const hipError_t e = hipLaunchKernel(fn, dim3(nb), dim3(gsm::roll_block_threads(p)), args, (unsigned)lds, s);
     if (e != hipSuccess) return hip_fail(h, e, "hipLaunchKernel (one-step rollout)");
     ++h->eager_launches;   // (only a launched step takes a half: a failed one leaves the order as it was)
     return GSM_OK;
@@ -948,7 +948,7 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
     hipError_t e = hipGetDevice(&dev);
     if (e == hipSuccess) e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
     if (e == hipSuccess)
-        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, roll_fn, gsm::block_threads(p), roll_lds);
+        e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, roll_fn, gsm::roll_block_threads(p), roll_lds);
     if (e != hipSuccess) return hip_fail(h, e, "occupancy query");
     if ((int64_t)per_cu * n_cu < nb) {
         if (fallback) return kRollIneligible;
@@ -1126,7 +1126,7 @@ static int capture_roll(gsm_handle *h, int32_t slot, const void *actions, int64_
         void *args[] = {&p};
         kp.func = const_cast<void *>(roll_fn);
         kp.gridDim = dim3(nb);
-        kp.blockDim = dim3(gsm::block_threads(p));
+        kp.blockDim = dim3(gsm::roll_block_threads(p));
         kp.sharedMemBytes = (unsigned)roll_lds;
         kp.kernelParams = args;
         kp.extra = nullptr;

@@ -241,6 +241,10 @@ const void *lag_step_ragged_kernel_fn();   // kLag: the previous step's emission
 const void *step_tile_kernel_fn();
 const void *emit_tile_kernel_fn();
 int block_threads(const DevParams &p);
+// threads per workgroup of the config's rollout kernel (the split packed
+// small-env rollout runs 512: four stepping and four emitting waves)
+int roll_block_threads(const DevParams &p);
+bool roll_pack_split(const DevParams &p);
 const void *emit_ragged_kernel_fn();
 // ragged path: per-device constant tables (unit circle, line fractions,
 // half-widths) computed on the host with libm; uploaded once per device.

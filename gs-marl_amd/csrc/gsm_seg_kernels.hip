@@ -2195,6 +2195,404 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     }
 }
 
+// ---------------------------------------------------------------------------
+// The same rollout of small envs with each stepping wave's edge emission on a
+// wave of its own (round 6; C2). gsm_roll_pack_kernel's waves are alone on
+// their SIMDs (C2's 1024 waves, one per SIMD) and each runs one serial chain
+// per step: ~2430 cycles of step, ~1900 of edge emission (15 scattered stores
+// per lane) and ~1650 settling the CSR offset (uncached granule loads under
+// load, profiles/r4_stamps/stamps_c2.json) — nothing hides any of it. Here a
+// workgroup holds its four stepping waves (the same 16 envs, the same per-wave
+// hand-off granules) and four emitting waves, one per stepper and on its SIMD:
+// a stepper publishes each step's positions (a ring of kPack2Ring LDS buffers)
+// and radius row bits (a ring of row words) and moves on; its emitter waits for
+// them, settles the offset (its loads for step j + 1 in flight while it emits
+// step j) and writes the edges. The two chains overlap. A stepper waits only
+// before reusing a ring slot its emitter has not finished (kPack2Ring - 2 steps
+// of slack); an emitter waits on its own stepper and, through the granules, on
+// steppers of lower index — every wait bounded (kRollSpinTicks, then the
+// sticky status word). Hand-offs between the two waves are LDS words: the data
+// written, lgkmcnt(0), then the count; the reader re-reads the count with
+// s_sleep and reads the data after it. Outputs, operations and their order are
+// gsm_roll_pack_kernel's (bit-identical: tests/test_gpu_roll.py).
+constexpr int kPack2Ring = 8;   // LDS ring slots: the stepper may run kPack2Ring - 2 steps ahead
+template <int kN, int kNo>
+constexpr int pack2_lds_stepper() {
+    return kPack2Ring * 8 * kPackG * (2 * kN + kNo) + 8 * kPackG * kN + kPack2Ring * 4 * kWave;
+}
+__device__ __forceinline__ int lds_count_ld(const volatile int *c) {
+    asm volatile("" ::: "memory");
+    const int v = *c;
+    asm volatile("" ::: "memory");
+    return v;
+}
+__device__ __forceinline__ void lds_count_st(volatile int *c, int v) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // the data before the count
+    *c = v;
+}
+// wait until *c >= want (wave-uniform); false if the bounded wait gave up
+__device__ __forceinline__ bool lds_count_wait(const volatile int *c, int want, uint32_t *status) {
+    if (__builtin_expect(lds_count_ld(c) >= want, 1)) return true;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        __builtin_amdgcn_s_sleep(1);
+        if (lds_count_ld(c) >= want) return true;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > kRollSpinTicks) {
+            if ((threadIdx.x & 63) == 0)
+                __hip_atomic_store((gu32 *)status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            return false;
+        }
+    }
+}
+
+template <int kN, int kNo, int kFmt, bool kSlots>
+__global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(4))) void gsm_roll_pack2_kernel(
+    DevParams p) {
+    constexpr int N = kN, M = kN + kNo, E = 2 * kN + kNo;
+    static_assert(M <= kPackSeg && E <= kPackSeg, "one 16-lane segment per env");
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const bool stepper = wv < kWavesPerBlock;
+    const int wave = stepper ? wv : wv - kWavesPerBlock;   // the stepper this wave is, or emits for
+    const int lane = threadIdx.x & 63, seg = lane >> 4, m = lane & (kPackSeg - 1);
+    const int64_t b = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kPackG + seg;   // this lane's env
+    const bool env_live = b < p.B;
+    const bool live = env_live && m < M, agent = live && m < N;
+    const int64_t eb = env_live ? b : 0;
+    // LDS per stepper: positions [kPack2Ring][G][E] (slot (j + 1) % ring holds
+    // the positions after step j, slot 0 those before the launch's first
+    // step), the next step's forces [G][N], radius row bits [kPack2Ring][64];
+    // then per stepper the steps published and the steps emitted
+    unsigned char *const s_st = smem + wave * pack2_lds_stepper<kN, kNo>();
+    float2 *const s_w = (float2 *)s_st;
+    auto pos_buf = [&](int i) { return s_w + i * kPackG * E + seg * E; };   // this env's rows in slot i
+    float2 *const s_force = s_w + kPack2Ring * kPackG * E + seg * N;
+    uint32_t *const s_rows = (uint32_t *)(s_w + kPack2Ring * kPackG * E + kPackG * N);
+    int *const s_bc = (int *)(smem + kWavesPerBlock * pack2_lds_stepper<kN, kNo>());   // [waves]
+    volatile int *const s_done = s_bc + kWavesPerBlock;       // [waves] steps published
+    volatile int *const s_emit = s_done + kWavesPerBlock;     // [waves] steps emitted
+    const int ent = m < N ? m : N + m;                        // this lane's collider entity
+    const int w = blockIdx.x * kWavesPerBlock + wave;        // the stepper's index in the grid (granules)
+    const int K = p.roll.K;
+    auto xf = [&]() -> Xfer {
+        KernargParams &q = late_params();
+        Xfer x;
+        x.W = q.roll.xW;
+        x.NG = q.roll.xNG;
+        x.agg = q.roll.gran;
+        x.grp = x.agg + (int64_t)q.roll.K * x.W;
+        x.status = q.roll.status;
+        x.etag = roll_epoch_tag(q.roll.epoch);
+        return x;
+    };
+    if (lane == 0 && stepper) {
+        s_done[wave] = 0;
+        s_emit[wave] = 0;
+    }
+    __syncthreads();
+
+    if (!stepper) {
+        // ---- the emitter: the edges of every step of its stepper's envs
+        auto emit = [&](const int j, const float2 *sp, const uint32_t row, const int woff) {
+            KernargParams &qs = late_params();
+            const int c = live ? __popc(row) + (agent ? 1 : 0) : 0;
+            const int incl = seg_scan16(c);
+            const int a_total = seg_sum16(agent ? c : 0);
+            const int e_tot = env_live ? seg_sum16(c) + N : 0;
+            const int t0 = __builtin_amdgcn_readlane(e_tot, 0), t1 = __builtin_amdgcn_readlane(e_tot, 16),
+                      t2 = __builtin_amdgcn_readlane(e_tot, 32);
+            const int before = (seg > 0 ? t0 : 0) + (seg > 1 ? t1 : 0) + (seg > 2 ? t2 : 0);
+            int64_t env_off = (int64_t)woff + before;
+            if (woff < 0) {   // a broken hand-off: never write out of bounds
+                if (lane == 0)
+                    __hip_atomic_store((gu32 *)qs.roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                env_off = qs.ro.cap;
+            }
+            if (env_live && m == 0) {
+                int64_t *const eptr = qs.ro.eptr + (kSlots ? j * qs.ro.ep_s : 0);
+                eptr[b] = env_off;
+                if (b == qs.B - 1) eptr[qs.B] = env_off + e_tot;
+            }
+            const EdgeSink out = roll_edge_sink<kSlots>(qs, j, K);
+            const int32_t g0 = (int32_t)(eb * E);
+            float2 qc[M];
+#pragma unroll
+            for (int cc = 0; cc < M; ++cc) qc[cc] = sp[cc < N ? cc : N + cc];
+            const float2 gq = sp[N + (m < N ? m : 0)];
+            const float2 a = sp[ent];
+            return [=](void) {
+                // (the positions are in registers here: the slot may be reused
+                // as soon as the emitted count is out)
+                if (!live) return;
+                int64_t o = env_off + (incl - c) + (m >= N ? N : 0);
+                auto put = [&](int64_t at, int dst, float2 qd) {
+                    if (at < out.cap) {
+                        const float dx = a.x - qd.x, dy = a.y - qd.y;
+                        out.index[at] = g0 + ent;
+                        out.index[out.cap + at] = g0 + dst;
+                        out.attr[at] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+                    }
+                };
+#pragma unroll
+                for (int cc = 0; cc < N; ++cc)
+                    if ((row >> cc) & 1u) put(o++, cc, qc[cc]);
+                if (agent) {
+                    put(o++, N + m, gq);                                 // agent m -> its goal
+                    const float dx = gq.x - a.x, dy = gq.y - a.y;
+                    const int64_t at = env_off + a_total + m;            // goal row: goal m -> agent m
+                    if (at < out.cap) {
+                        out.index[at] = g0 + N + m;
+                        out.index[out.cap + at] = g0 + m;
+                        out.attr[at] = __builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+                    }
+                }
+#pragma unroll
+                for (int cc = N; cc < M; ++cc)
+                    if ((row >> cc) & 1u) put(o++, N + cc, qc[cc]);
+            };
+        };
+        XferOff xo = xfer_off_load_all(xf(), 0, w, lane);
+        for (int j = 0; j < K; ++j) {
+            if (!lds_count_wait(s_done + wave, j + 1, late_params().roll.status)) break;
+            const uint32_t row = s_rows[(j % kPack2Ring) * kWave + lane];
+            const int woff = xfer_off_settle(xf(), xo, j, w, lane);
+            // the next step's offset loads, in flight during this emission
+            xo = xfer_off_load_all(xf(), j + 1 < K ? j + 1 : j, w, lane);
+            auto write = emit(j, pos_buf((j + 1) % kPack2Ring), row, woff);
+            if (lane == 0) lds_count_st(s_emit + wave, j + 1);   // the slot's positions are in registers
+            write();
+        }
+    } else {
+        // ---- the stepper: gsm_roll_pack_kernel's loop without the emission
+        const float2 *pos_g = p.pos + eb * E;
+        float2 x = env_live && m < E ? pos_g[m] : make_float2(0.0f, 0.0f);
+        float2 v = agent ? p.vel[eb * N + m] : make_float2(0.0f, 0.0f);
+        int t = env_live ? p.step_count[eb] : 0, ep = env_live ? p.episode[eb] : 0;
+        float2 acc = env_live ? p.ep_acc[eb] : make_float2(0.0f, 0.0f);
+        uint32_t cand_prev = agent ? (uint32_t)p.contact_mask[eb * N + m] : 0u;
+        const float4 a0 = roll_action_load<kN, kFmt>(p, p.roll.t_first % p.roll.n_actions, eb, agent ? m : 0);
+        if (env_live && m < E) pos_buf(0)[m] = x;
+        wave_sync();
+        auto sweep = [&](const float2 *sp, float2 pm, uint32_t &rad, uint32_t &cand, int &cnt, bool &zero_agent,
+                         float2 *F) {
+            KernargParams &q = late_params();
+            uint32_t r2b1 = __float_as_uint(q.R2) + 1u;
+            asm volatile("" : "+v"(r2b1));
+            uint32_t cut_aa = __float_as_uint(q.cut2_aa), cut_ao = __float_as_uint(q.cut2_ao);
+            asm volatile("" : "+v"(cut_aa), "+v"(cut_ao));
+            uint32_t rw = 0, cw = 0, nz = 0;
+#pragma unroll
+            for (int c = M - 1; c >= 0; --c) {
+                const float2 qc = sp[c < N ? c : N + c];
+                const float dx = pm.x - qc.x, dy = pm.y - qc.y;
+                const uint32_t a = __float_as_uint(__builtin_fabsf(dx * dx) + __builtin_fabsf(dy * dy));
+                const uint32_t na = 0u - a;
+                const uint32_t cb = (c < N && m < N) ? cut_aa : cut_ao;
+                rw = __builtin_amdgcn_alignbit(rw, na & (a - r2b1), 31);
+                cw = __builtin_amdgcn_alignbit(cw, na & (a - cb), 31);
+                nz = __builtin_amdgcn_alignbit(nz, na, 31);
+            }
+            constexpr uint32_t colmask = (1u << M) - 1u, amask = (1u << N) - 1u;
+            const uint32_t self = 1u << m;
+            const uint32_t zero = ~nz & colmask & ~self;
+            zero_agent = live && (zero & amask) != 0u;
+            rad = live ? rw & colmask : 0u;
+            cand = agent ? cw & colmask : 0u;
+            int n = agent ? __popc(zero) : 0;
+            if (agent) {
+                float Fx = F ? F->x : 0.0f, Fy = F ? F->y : 0.0f;
+                const float dmin2_aa = q.dmin2_aa, dmin2_ao = q.dmin2_ao, dmin_aa = q.dmin_aa, dmin_ao = q.dmin_ao;
+                for (uint32_t wd = cand; wd; wd &= wd - 1u) {
+                    const int c = __builtin_ctz(wd);
+                    const bool ag = c < N;
+                    const float2 qc = sp[ag ? c : N + c];
+                    const float dx = pm.x - qc.x, dy = pm.y - qc.y;
+                    const float d2 = dx * dx + dy * dy;
+                    n += d2 < (ag ? dmin2_aa : dmin2_ao) ? 1 : 0;
+                    if (F) {
+                        const float f = contact_scale(q, d2, ag ? dmin_aa : dmin_ao);
+                        Fx += f * dx;
+                        Fy += f * dy;
+                    }
+                }
+                if (F) *F = make_float2(Fx, Fy);
+            }
+            cnt = n;
+        };
+        {   // the forces of step t_first: its action, then the stored candidates
+            float2 F = roll_force<kFmt>(late_params(), a0, agent);
+            if (agent) {
+                const float2 pi = x;
+                const float dmin_aa = late_params().dmin_aa, dmin_ao = late_params().dmin_ao;
+                for (uint32_t wd = cand_prev; wd; wd &= wd - 1u) {
+                    const int c = __builtin_ctz(wd);
+                    const bool ag = c < N;
+                    const float2 pj = pos_buf(0)[ag ? c : N + c];
+                    const float dx = pi.x - pj.x, dy = pi.y - pj.y;
+                    const float d2 = dx * dx + dy * dy;
+                    const float f = contact_scale(late_params(), d2, ag ? dmin_aa : dmin_ao);
+                    F.x += f * dx;
+                    F.y += f * dy;
+                }
+                s_force[m] = F;
+            }
+        }
+        const int n_act = p.roll.n_actions;
+        int arow = p.roll.t_first % n_act;
+        const bool glast = (w & 63) == 63;
+        int cnt_m1 = 0, cnt_m2 = 0;
+        uint32_t cand_keep = cand_prev, last_row = 0;
+        bool coinc = false;
+        int nrow = arow + 1 == n_act ? 0 : arow + 1;
+        float4 anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, agent ? m : 0);
+        uint64_t gl = xfer_grp_load(xf(), 0, w, lane);
+        for (int k = 0; k < K; ++k) {
+            const float2 *const s_cur = pos_buf(k % kPack2Ring);
+            float2 *const s_pos = pos_buf((k + 1) % kPack2Ring);
+            // the slot about to be written held step k + 1 - ring's positions:
+            // emitted before it is reused
+            if (k + 2 - kPack2Ring > 0) (void)lds_count_wait(s_emit + wave, k + 2 - kPack2Ring, late_params().roll.status);
+            KernargParams &pc = late_params();
+            if (agent) {
+                const float2 pi = s_cur[m];
+                const float2 F0 = s_force[m];
+                float Fx = F0.x, Fy = F0.y;
+                if (pc.strict && strict_bad(m, pi, N, M, [&](int c) { return s_cur[c < N ? c : N + c]; })) {
+                    Fx = __builtin_nanf("");
+                    Fy = __builtin_nanf("");
+                }
+                const float dt = pc.dt, max_speed = pc.max_speed;
+                v.x = v.x * pc.omd;
+                v.y = v.y * pc.omd;
+                v.x = v.x + (Fx * pc.inv_mass) * dt;
+                v.y = v.y + (Fy * pc.inv_mass) * dt;
+                if (max_speed > 0.0f) {
+                    const float sp = sqrtf(v.x * v.x + v.y * v.y);
+                    if (sp > max_speed) {
+                        v.x = v.x / sp * max_speed;
+                        v.y = v.y / sp * max_speed;
+                    }
+                }
+                s_pos[m] = make_float2(pi.x + v.x * dt, pi.y + v.y * dt);
+            } else if (env_live && m < E) {
+                s_pos[m] = s_cur[m];
+            }
+            wave_sync();
+            t += 1;
+            const bool done = env_live && t >= pc.EL;
+            float2 pm = live ? s_pos[ent] : make_float2(0.0f, 0.0f);
+            uint32_t rad, cand;
+            int cnt;
+            bool za;
+            float2 Fn = roll_force<kFmt>(late_params(), anext, agent);
+            sweep(s_pos, pm, rad, cand, cnt, za, &Fn);
+            float r = 0.0f;
+            if (agent) {
+                const float2 g = s_pos[N + m];
+                const float dx = pm.x - g.x, dy = pm.y - g.y;
+                r = -__builtin_amdgcn_sqrtf(dx * dx + dy * dy);
+            }
+            float rsum = seg_sum16(r);
+            const int csum = seg_sum16(agent ? cnt : 0);
+            {
+                KernargParams &q = late_params();
+                if (agent) {
+                    (q.ro.rew + (kSlots ? k * q.ro.rc_s : 0) + eb * N)[m] = q.shared_reward ? rsum : r;
+                    (q.ro.cost + (kSlots ? k * q.ro.rc_s : 0) + eb * N)[m] = (float)cnt;
+                }
+                if (q.shared_reward) rsum *= (float)N;
+            }
+            if (env_live) {
+                acc.x += rsum;
+                acc.y += (float)csum;
+            }
+            const bool reset = done && late_params().auto_reset;
+            if (reset && m == 0) late_params().ep_last[b] = acc;
+            if (__any(reset)) {
+                if (reset) {
+                    ep = ep + 1;
+                    t = 0;
+                    acc = make_float2(0.0f, 0.0f);
+                    v = make_float2(0.0f, 0.0f);
+                    const uint32_t gid = (uint32_t)(late_params().env_base + b);
+                    if (m < E) s_pos[m] = layout_pos(p, gid, (uint32_t)ep, (uint32_t)m);
+                }
+                wave_sync();
+                if (reset) {
+                    pm = live ? s_pos[ent] : make_float2(0.0f, 0.0f);
+                    Fn = roll_force<kFmt>(late_params(), anext, agent);
+                    sweep(s_pos, pm, rad, cand, cnt, za, &Fn);
+                }
+            }
+            coinc = (seg_sum16(za ? 1 : 0) != 0);
+            if (agent) s_force[m] = Fn;
+            // the step's row bits for the emitter, then the step published to it
+            s_rows[(k % kPack2Ring) * kWave + lane] = rad;
+            if (lane == 0) lds_count_st(s_done + wave, k + 1);
+            KernargParams &q = late_params();
+            const bool statics = q.nf_full || reset;
+            float *nf = q.ro.nf + (kSlots ? k * q.ro.nf_s : 0) + eb * E * 7;
+            if (agent) {
+                const float2 g = s_pos[N + m];
+                store_row(nf + m * 7, v, pm, make_float2(g.x - pm.x, g.y - pm.y), 0.0f);
+            }
+            if (env_live && statics && m >= N && m < E) {
+                const float2 a = s_pos[m];
+                store_row(nf + m * 7, make_float2(0.0f, 0.0f), a, make_float2(0.0f, 0.0f), m < 2 * N ? 1.0f : 2.0f);
+            }
+            const int edges = seg_sum16(live ? (int)__popc(rad) : 0) + 2 * N;
+            if (env_live && m == 0) {
+                (q.ro.done + (kSlots ? k * q.ro.done_s : 0))[b] = done ? 1 : 0;
+                if (kSlots || k == K - 1) (q.ro.ecount + (kSlots ? k * q.ro.ec_s : 0))[b] = edges;
+            }
+            const int ev = env_live ? edges : 0;
+            const int wcnt = __builtin_amdgcn_readlane(ev, 0) + __builtin_amdgcn_readlane(ev, 16) +
+                             __builtin_amdgcn_readlane(ev, 32) + __builtin_amdgcn_readlane(ev, 48);
+            if (lane == 0) xfer_st(xf().agg + (int64_t)k * xf().W + w, xf().tag(k), (uint32_t)wcnt);
+            if (k >= 2 && glast) xfer_grp_publish(xf(), gl, k - 2, w, lane, cnt_m2);
+            cnt_m2 = cnt_m1;
+            cnt_m1 = wcnt;
+            cand_keep = cand;
+            last_row = rad;
+            arow = nrow;
+            nrow = arow + 1 == n_act ? 0 : arow + 1;
+            anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, agent ? m : 0);
+            gl = xfer_grp_load(xf(), k + 1 >= 2 ? k - 1 : 0, w, lane);
+            wave_sync();
+        }
+        // the group sums of the last two steps (the first's load issued by the loop)
+        for (int k = K; k < K + 2; ++k) {
+            if (k > K) gl = xfer_grp_load(xf(), min(max(k - 2, 0), K - 1), w, lane);
+            if (k - 2 >= 0 && k - 2 < K && glast) xfer_grp_publish(xf(), gl, k - 2, w, lane, cnt_m2);
+            cnt_m2 = cnt_m1;
+        }
+        // the final state (what the next launch or an eager step reads)
+        KernargParams &q = late_params();
+        const float2 *const s_fin = pos_buf(K % kPack2Ring);
+        if (env_live && m < E) q.pos[eb * E + m] = s_fin[m];
+        if (agent) {
+            q.vel[eb * N + m] = v;
+            q.contact_mask[eb * N + m] = cand_keep;
+        }
+        if (live) q.row_mask[eb * M + m] = last_row;
+        if (env_live && m == 0) {
+            q.step_count[b] = t;
+            q.episode[b] = ep;
+            q.ep_acc[b] = acc;
+        }
+        if (q.degenerate) {
+            const bool nf_agent = agent && nonfinite2(s_fin[m]);
+            const bool nfe = seg_sum16(nf_agent ? 1 : 0) != 0;
+            if (env_live && m == 0) q.degenerate[b] = (uint8_t)((coinc ? kDegCoincident : 0) | (nfe ? kDegNonfinite : 0));
+        }
+        if (lane == 0) s_bc[wave] = cnt_m1;   // the last step's count (cnt_m1 = cnt of step K - 1 before the shift)
+    }
+    // the last step's sums in the config's workgroup layout (G = 4: the same
+    // 16 envs per workgroup), for the emit launch that may follow
+    __syncthreads();
+    if (threadIdx.x == 0 && K >= 1) late_params().block_edge_sum[blockIdx.x] = s_bc[0] + s_bc[1] + s_bc[2] + s_bc[3];
+}
+
 // Specialisations with compile-time shapes (segment arithmetic folded, G = 1
 // collectives for 24 agents) and action formats; anything else runs the
 // runtime-shape instantiation.
@@ -2229,19 +2627,35 @@ bool roll_packed(const DevParams &p) {
     return false;
 }
 int roll_seg_envs_per_block(const DevParams &p) { return roll_packed(p) ? kWavesPerBlock * kPackG : kWavesPerBlock; }
+// the packed small-env rollout with its emission on waves of its own
+// (gsm_roll_pack2_kernel: 512-thread workgroups, two per CU at most, so up to
+// 8192 envs in one residency round; larger batches keep gsm_roll_pack_kernel;
+// GSM_PACK_SPLIT=0 keeps it everywhere, an A/B knob)
+bool roll_pack_split(const DevParams &p) {
+    static const bool on = [] {
+        const char *e = getenv("GSM_PACK_SPLIT");
+        return !(e && *e && atoi(e) == 0);
+    }();
+    return on && roll_packed(p) && p.B <= 512 * kWavesPerBlock * kPackG;
+}
+int roll_block_threads(const DevParams &p) { return roll_pack_split(p) ? 2 * kBlock : block_threads(p); }
 
 template <bool kSlots, bool kEager = false>
 static const void *pick_roll_seg(const DevParams &p) {
     if constexpr (kEager) {   // (one env per wave only: the packed rollout keeps host epochs)
         if (roll_packed(p)) return nullptr;
     } else {
-#define GSM_PICK(n, no)                                                                            \
-    if (p.N == n && p.No == no) {                                                                  \
-        switch (p.action_fmt) {                                                                    \
-            case 0: return reinterpret_cast<const void *>(&gsm_roll_pack_kernel<n, no, 0, kSlots>); \
-            case 1: return reinterpret_cast<const void *>(&gsm_roll_pack_kernel<n, no, 1, kSlots>); \
-            default: return reinterpret_cast<const void *>(&gsm_roll_pack_kernel<n, no, 2, kSlots>); \
-        }                                                                                          \
+        const bool split = roll_pack_split(p);
+#define GSM_PICK(n, no)                                                                                     \
+    if (p.N == n && p.No == no) {                                                                           \
+        switch (p.action_fmt) {                                                                             \
+            case 0: return split ? reinterpret_cast<const void *>(&gsm_roll_pack2_kernel<n, no, 0, kSlots>)  \
+                                 : reinterpret_cast<const void *>(&gsm_roll_pack_kernel<n, no, 0, kSlots>);  \
+            case 1: return split ? reinterpret_cast<const void *>(&gsm_roll_pack2_kernel<n, no, 1, kSlots>)  \
+                                 : reinterpret_cast<const void *>(&gsm_roll_pack_kernel<n, no, 1, kSlots>);  \
+            default: return split ? reinterpret_cast<const void *>(&gsm_roll_pack2_kernel<n, no, 2, kSlots>) \
+                                  : reinterpret_cast<const void *>(&gsm_roll_pack_kernel<n, no, 2, kSlots>); \
+        }                                                                                                   \
     }
         GSM_PACK_SHAPES(GSM_PICK)
 #undef GSM_PICK
@@ -2267,8 +2681,10 @@ const void *roll_seg_eager_kernel_fn(const DevParams &p) {
     return pick_roll_seg<false, true>(p);
 }
 size_t roll_kernel_lds(const DevParams &p) {
-#define GSM_PICK(n, no) \
-    if (p.N == n && p.No == no) return (size_t)kWavesPerBlock * pack_lds_wave<n, no>() + 4 * kWavesPerBlock;
+#define GSM_PICK(n, no)                                                                             \
+    if (p.N == n && p.No == no)                                                                     \
+        return roll_pack_split(p) ? (size_t)kWavesPerBlock * pack2_lds_stepper<n, no>() + 12 * kWavesPerBlock \
+                                  : (size_t)kWavesPerBlock * pack_lds_wave<n, no>() + 4 * kWavesPerBlock;
     GSM_PACK_SHAPES(GSM_PICK)
 #undef GSM_PICK
     return (size_t)kWavesPerBlock * roll_lds_wave(p.N, p.E) + 4 * (6 * kWavesPerBlock + 4);
