@@ -2216,6 +2216,13 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
 // s_sleep and reads the data after it. Outputs, operations and their order are
 // gsm_roll_pack_kernel's (bit-identical: tests/test_gpu_roll.py).
 constexpr int kPack2Ring = 8;   // LDS ring slots: the stepper may run kPack2Ring - 2 steps ahead
+#ifndef GSM_PACK2_APREF
+#define GSM_PACK2_APREF 3   // steps of actions in flight in a stepper
+#endif
+#ifndef GSM_PACK2_LAG
+#define GSM_PACK2_LAG 3   // steps the stepper is ahead when its emitter starts a step (< kPack2Ring - 2)
+#endif
+static_assert(GSM_PACK2_LAG + 2 < kPack2Ring, "the stepper must not wait for its lagging emitter");
 template <int kN, int kNo>
 constexpr int pack2_lds_stepper() {
     return kPack2Ring * 8 * kPackG * (2 * kN + kNo) + 8 * kPackG * kN + kPack2Ring * 4 * kWave;
@@ -2290,6 +2297,10 @@ __global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
         s_emit[wave] = 0;
     }
     __syncthreads();
+    // (diagnostic stamps, tools/stamps_c2_roll.py: per stepper wave w, slots
+    // 0-2 its step / publish / ring wait, 3-5 its emitter's wait for the step /
+    // offset settle / emission, 8-11 start and end of both)
+    GSM_RSTAMP(p, w, stepper ? 8 : 10);
 
     if (!stepper) {
         // ---- the emitter: the edges of every step of its stepper's envs
@@ -2351,17 +2362,29 @@ __global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
                     if ((row >> cc) & 1u) put(o++, N + cc, qc[cc]);
             };
         };
+        // Step j is emitted once the stepper has finished step j + kPack2Lag
+        // (or the launch's last): the group sums of step j + 1, published by
+        // the groups' last steppers in their iteration j + 3, are then normally
+        // complete when this emission's loads for step j + 1 are issued, so the
+        // next settle does not re-poll a granule (an uncached round trip each)
         XferOff xo = xfer_off_load_all(xf(), 0, w, lane);
         for (int j = 0; j < K; ++j) {
-            if (!lds_count_wait(s_done + wave, j + 1, late_params().roll.status)) break;
+            GSM_TNOW(te0);
+            if (!lds_count_wait(s_done + wave, min(j + 1 + GSM_PACK2_LAG, K), late_params().roll.status)) break;
+            GSM_ACC(late_params(), w, 3, te0);
+            GSM_TNOW(te1);
             const uint32_t row = s_rows[(j % kPack2Ring) * kWave + lane];
             const int woff = xfer_off_settle(xf(), xo, j, w, lane);
+            GSM_ACC(late_params(), w, 5, te1);
+            GSM_TNOW(te2);
             // the next step's offset loads, in flight during this emission
             xo = xfer_off_load_all(xf(), j + 1 < K ? j + 1 : j, w, lane);
             auto write = emit(j, pos_buf((j + 1) % kPack2Ring), row, woff);
             if (lane == 0) lds_count_st(s_emit + wave, j + 1);   // the slot's positions are in registers
             write();
+            GSM_ACC(late_params(), w, 4, te2);
         }
+        GSM_RSTAMP(p, w, 11);
     } else {
         // ---- the stepper: gsm_roll_pack_kernel's loop without the emission
         const float2 *pos_g = p.pos + eb * E;
@@ -2443,15 +2466,28 @@ __global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
         int cnt_m1 = 0, cnt_m2 = 0;
         uint32_t cand_keep = cand_prev, last_row = 0;
         bool coinc = false;
-        int nrow = arow + 1 == n_act ? 0 : arow + 1;
-        float4 anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, agent ? m : 0);
+        // The next steps' actions are loaded GSM_PACK2_APREF steps ahead: in
+        // gsm_roll_pack_kernel the emission filled the time between an action
+        // load and its use in the next iteration's sweep; without it a load one
+        // step ahead would be waited for every step (an HBM round trip)
+        float4 apf[GSM_PACK2_APREF];
+        int prow = arow;   // the row of the last prefetched step
+#pragma unroll
+        for (int d = 0; d < GSM_PACK2_APREF; ++d) {
+            prow = prow + 1 == n_act ? 0 : prow + 1;
+            apf[d] = roll_action_load<kN, kFmt>(late_params(), prow, eb, agent ? m : 0);
+        }
         uint64_t gl = xfer_grp_load(xf(), 0, w, lane);
         for (int k = 0; k < K; ++k) {
+            const float4 anext = apf[0];   // step k + 1's actions
             const float2 *const s_cur = pos_buf(k % kPack2Ring);
             float2 *const s_pos = pos_buf((k + 1) % kPack2Ring);
             // the slot about to be written held step k + 1 - ring's positions:
             // emitted before it is reused
+            GSM_TNOW(tw0);
             if (k + 2 - kPack2Ring > 0) (void)lds_count_wait(s_emit + wave, k + 2 - kPack2Ring, late_params().roll.status);
+            GSM_ACC(late_params(), w, 2, tw0);
+            GSM_TNOW(tc0);
             KernargParams &pc = late_params();
             if (agent) {
                 const float2 pi = s_cur[m];
@@ -2548,15 +2584,19 @@ __global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
             const int ev = env_live ? edges : 0;
             const int wcnt = __builtin_amdgcn_readlane(ev, 0) + __builtin_amdgcn_readlane(ev, 16) +
                              __builtin_amdgcn_readlane(ev, 32) + __builtin_amdgcn_readlane(ev, 48);
+            GSM_ACC(late_params(), w, 0, tc0);
+            GSM_TNOW(tc1);
             if (lane == 0) xfer_st(xf().agg + (int64_t)k * xf().W + w, xf().tag(k), (uint32_t)wcnt);
             if (k >= 2 && glast) xfer_grp_publish(xf(), gl, k - 2, w, lane, cnt_m2);
+            GSM_ACC(late_params(), w, 1, tc1);
             cnt_m2 = cnt_m1;
             cnt_m1 = wcnt;
             cand_keep = cand;
             last_row = rad;
-            arow = nrow;
-            nrow = arow + 1 == n_act ? 0 : arow + 1;
-            anext = roll_action_load<kN, kFmt>(late_params(), nrow, eb, agent ? m : 0);
+#pragma unroll
+            for (int d = 0; d + 1 < GSM_PACK2_APREF; ++d) apf[d] = apf[d + 1];
+            prow = prow + 1 == n_act ? 0 : prow + 1;
+            apf[GSM_PACK2_APREF - 1] = roll_action_load<kN, kFmt>(late_params(), prow, eb, agent ? m : 0);
             gl = xfer_grp_load(xf(), k + 1 >= 2 ? k - 1 : 0, w, lane);
             wave_sync();
         }
@@ -2585,7 +2625,8 @@ __global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
             const bool nfe = seg_sum16(nf_agent ? 1 : 0) != 0;
             if (env_live && m == 0) q.degenerate[b] = (uint8_t)((coinc ? kDegCoincident : 0) | (nfe ? kDegNonfinite : 0));
         }
-        if (lane == 0) s_bc[wave] = cnt_m1;   // the last step's count (cnt_m1 = cnt of step K - 1 before the shift)
+        if (lane == 0) s_bc[wave] = cnt_m1;   // the last step's count
+        GSM_RSTAMP(p, w, 9);
     }
     // the last step's sums in the config's workgroup layout (G = 4: the same
     // 16 envs per workgroup), for the emit launch that may follow

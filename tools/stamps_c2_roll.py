@@ -38,6 +38,20 @@ s1.record()
 torch.cuda.synchronize()
 assert not env.roll_gave_up()
 q = st.cpu().numpy().astype(np.int64)
+if q[:, 10].any():   # gsm_roll_pack2_kernel: stepping and emitting waves
+    t0 = min(q[:, 8].min(), q[:, 10].min())
+    names = {0: "step_work", 1: "publish", 2: "ring_wait", 3: "emitter_wait_step", 5: "emitter_offset_settle",
+             4: "emitter_emit"}
+    out = {"launch_ms_events": s0.elapsed_time(s1),
+           "stepper_span_us_max": float(((q[:, 9] - t0) / 100.0).max()),
+           "emitter_span_us_max": float(((q[:, 11] - t0) / 100.0).max()),
+           "stepper_end_us_p50": float(np.median((q[:, 9] - t0) / 100.0)),
+           "emitter_end_us_p50": float(np.median((q[:, 11] - t0) / 100.0)),
+           "cycles_per_step_mean": {n: float(q[:, i].mean() / T) for i, n in names.items()},
+           "cycles_per_step_p99": {n: float(np.percentile(q[:, i] / T, 99)) for i, n in names.items()}}
+    print(json.dumps(out, indent=1))
+    env.close()
+    sys.exit(0)
 names = ["work", "publish", "unused", "offset_settle", "emit"]
 t0 = q[:, 8].min()
 start, end = (q[:, 8] - t0) / 100.0, (q[:, 9] - t0) / 100.0
