@@ -2223,6 +2223,11 @@ constexpr int kPack2Ring = 8;   // LDS ring slots: the stepper may run kPack2Rin
 #define GSM_PACK2_LAG 3   // steps the stepper is ahead when its emitter starts a step (< kPack2Ring - 2)
 #endif
 static_assert(GSM_PACK2_LAG + 2 < kPack2Ring, "the stepper must not wait for its lagging emitter");
+#ifndef GSM_PACK2_EMITTERS
+#define GSM_PACK2_EMITTERS 1   // emitting waves per stepping wave (steps dealt round robin; 2: 2.43, 3: 2.50 vs 2.29 us, profiles/r6_ab/c2_emitters)
+#endif
+constexpr int kPack2Emitters = GSM_PACK2_EMITTERS;
+constexpr int kPack2Block = kWave * kWavesPerBlock * (1 + kPack2Emitters);
 template <int kN, int kNo>
 constexpr int pack2_lds_stepper() {
     return kPack2Ring * 8 * kPackG * (2 * kN + kNo) + 8 * kPackG * kN + kPack2Ring * 4 * kWave;
@@ -2253,14 +2258,19 @@ __device__ __forceinline__ bool lds_count_wait(const volatile int *c, int want, 
 }
 
 template <int kN, int kNo, int kFmt, bool kSlots>
-__global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(4))) void gsm_roll_pack2_kernel(
+// (two workgroups per CU: 8192 envs in one residency round)
+__global__ __launch_bounds__(kPack2Block) __attribute__((amdgpu_waves_per_eu(2 * (1 + kPack2Emitters)))) void
+gsm_roll_pack2_kernel(
     DevParams p) {
     constexpr int N = kN, M = kN + kNo, E = 2 * kN + kNo;
     static_assert(M <= kPackSeg && E <= kPackSeg, "one 16-lane segment per env");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const bool stepper = wv < kWavesPerBlock;
-    const int wave = stepper ? wv : wv - kWavesPerBlock;   // the stepper this wave is, or emits for
+    // emitter (wv - 4) serves stepper (wv - 4) % 4 and emits its steps
+    // j = par (mod kPack2Emitters)
+    const int wave = stepper ? wv : (wv - kWavesPerBlock) % kWavesPerBlock;   // the stepper this wave is, or emits for
+    const int par = stepper ? 0 : (wv - kWavesPerBlock) / kWavesPerBlock;
     const int lane = threadIdx.x & 63, seg = lane >> 4, m = lane & (kPackSeg - 1);
     const int64_t b = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kPackG + seg;   // this lane's env
     const bool env_live = b < p.B;
@@ -2277,7 +2287,7 @@ __global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
     uint32_t *const s_rows = (uint32_t *)(s_w + kPack2Ring * kPackG * E + kPackG * N);
     int *const s_bc = (int *)(smem + kWavesPerBlock * pack2_lds_stepper<kN, kNo>());   // [waves]
     volatile int *const s_done = s_bc + kWavesPerBlock;       // [waves] steps published
-    volatile int *const s_emit = s_done + kWavesPerBlock;     // [waves] steps emitted
+    volatile int *const s_emit = s_done + kWavesPerBlock;     // [waves][emitters] last step emitted + 1
     const int ent = m < N ? m : N + m;                        // this lane's collider entity
     const int w = blockIdx.x * kWavesPerBlock + wave;        // the stepper's index in the grid (granules)
     const int K = p.roll.K;
@@ -2294,7 +2304,7 @@ __global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
     };
     if (lane == 0 && stepper) {
         s_done[wave] = 0;
-        s_emit[wave] = 0;
+        for (int e = 0; e < kPack2Emitters; ++e) s_emit[wave * kPack2Emitters + e] = 0;
     }
     __syncthreads();
     // (diagnostic stamps, tools/stamps_c2_roll.py: per stepper wave w, slots
@@ -2319,7 +2329,10 @@ __global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
                     __hip_atomic_store((gu32 *)qs.roll.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 env_off = qs.ro.cap;
             }
-            if (env_live && m == 0) {
+            // (the bound edge_ptr holds the last step's offsets: with several
+            // emitters per stepper an earlier step's could land after it, so
+            // in the bound buffers only the last step writes them)
+            if (env_live && m == 0 && (kSlots || j == K - 1)) {
                 int64_t *const eptr = qs.ro.eptr + (kSlots ? j * qs.ro.ep_s : 0);
                 eptr[b] = env_off;
                 if (b == qs.B - 1) eptr[qs.B] = env_off + e_tot;
@@ -2367,8 +2380,8 @@ __global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
         // the groups' last steppers in their iteration j + 3, are then normally
         // complete when this emission's loads for step j + 1 are issued, so the
         // next settle does not re-poll a granule (an uncached round trip each)
-        XferOff xo = xfer_off_load_all(xf(), 0, w, lane);
-        for (int j = 0; j < K; ++j) {
+        XferOff xo = xfer_off_load_all(xf(), par < K ? par : 0, w, lane);
+        for (int j = par; j < K; j += kPack2Emitters) {
             GSM_TNOW(te0);
             if (!lds_count_wait(s_done + wave, min(j + 1 + GSM_PACK2_LAG, K), late_params().roll.status)) break;
             GSM_ACC(late_params(), w, 3, te0);
@@ -2378,9 +2391,9 @@ __global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
             GSM_ACC(late_params(), w, 5, te1);
             GSM_TNOW(te2);
             // the next step's offset loads, in flight during this emission
-            xo = xfer_off_load_all(xf(), j + 1 < K ? j + 1 : j, w, lane);
+            xo = xfer_off_load_all(xf(), j + kPack2Emitters < K ? j + kPack2Emitters : j, w, lane);
             auto write = emit(j, pos_buf((j + 1) % kPack2Ring), row, woff);
-            if (lane == 0) lds_count_st(s_emit + wave, j + 1);   // the slot's positions are in registers
+            if (lane == 0) lds_count_st(s_emit + wave * kPack2Emitters + par, j + 1);   // positions in registers
             write();
             GSM_ACC(late_params(), w, 4, te2);
         }
@@ -2485,7 +2498,11 @@ __global__ __launch_bounds__(2 * kBlock) __attribute__((amdgpu_waves_per_eu(4)))
             // the slot about to be written held step k + 1 - ring's positions:
             // emitted before it is reused
             GSM_TNOW(tw0);
-            if (k + 2 - kPack2Ring > 0) (void)lds_count_wait(s_emit + wave, k + 2 - kPack2Ring, late_params().roll.status);
+            if (k >= kPack2Ring) {   // step k - ring, emitted by emitter (k - ring) mod emitters
+                const int jo = k - kPack2Ring;
+                (void)lds_count_wait(s_emit + wave * kPack2Emitters + jo % kPack2Emitters, jo + 1,
+                                     late_params().roll.status);
+            }
             GSM_ACC(late_params(), w, 2, tw0);
             GSM_TNOW(tc0);
             KernargParams &pc = late_params();
@@ -2679,7 +2696,7 @@ bool roll_pack_split(const DevParams &p) {
     }();
     return on && roll_packed(p) && p.B <= 512 * kWavesPerBlock * kPackG;
 }
-int roll_block_threads(const DevParams &p) { return roll_pack_split(p) ? 2 * kBlock : block_threads(p); }
+int roll_block_threads(const DevParams &p) { return roll_pack_split(p) ? kPack2Block : block_threads(p); }
 
 template <bool kSlots, bool kEager = false>
 static const void *pick_roll_seg(const DevParams &p) {
@@ -2724,7 +2741,7 @@ const void *roll_seg_eager_kernel_fn(const DevParams &p) {
 size_t roll_kernel_lds(const DevParams &p) {
 #define GSM_PICK(n, no)                                                                             \
     if (p.N == n && p.No == no)                                                                     \
-        return roll_pack_split(p) ? (size_t)kWavesPerBlock * pack2_lds_stepper<n, no>() + 12 * kWavesPerBlock \
+        return roll_pack_split(p) ? (size_t)kWavesPerBlock * pack2_lds_stepper<n, no>() + 4 * kWavesPerBlock * (2 + kPack2Emitters) \
                                   : (size_t)kWavesPerBlock * pack_lds_wave<n, no>() + 4 * kWavesPerBlock;
     GSM_PACK_SHAPES(GSM_PICK)
 #undef GSM_PICK
