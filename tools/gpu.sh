@@ -110,7 +110,7 @@ case $CMD in
     bash tools/gpu.sh pmc $T || exit 1
     bash tools/gpu.sh tests $T || exit 2
     bash tools/gpu.sh lines $T || exit 4
-    bash tools/gpu.sh prof $T h c4 eager policyg buffer || exit 6 ;;
+    bash tools/gpu.sh prof $T h c4 c2 eager policygc buffer || exit 6 ;;
   ab)
     for rep in 1 2; do
       for v in lib "$@"; do
