@@ -384,6 +384,9 @@ def parse_args(argv=None):
     ap.add_argument("--policy-graph", action="store_true",
                     help="the closed loop of --policy with the policy and env.step captured into one "
                          "torch.cuda graph per step (replayed every step)")
+    ap.add_argument("--policy-graph-steps", type=int, default=1,
+                    help="--policy-graph: steps of policy + env.step captured in the one graph (a runner "
+                         "collecting a rollout on device replays one graph per S steps)")
     ap.add_argument("--policy-act", choices=("index", "cont"), default="index",
                     help="--policy / --policy-graph action format: index = the greedy discrete action (int32, "
                          "three small kernels), cont = the continuous bang-bang action sign(goal - position) "
@@ -634,7 +637,8 @@ def run_rank(args):
         torch.cuda.current_stream().wait_stream(side)
         pgraph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(pgraph):
-            venv.step(greedy(obs))   # obs: a view of the env's node features, static
+            for _ in range(args.policy_graph_steps):   # S steps of policy + env.step per replay
+                venv.step(greedy(obs))   # obs: a view of the env's node features, static
 
     host_actions = actions.cpu().numpy() if args.vec_env else None
     vec_t = 0
@@ -642,8 +646,11 @@ def run_rank(args):
     def run_steps(n, slot):
         nonlocal obs, vec_t
         if pgraph is not None:
-            for t in range(n):
+            S = args.policy_graph_steps
+            for t in range(n // S):
                 pgraph.replay()
+            for t in range(n % S):   # (a remainder: eager policy + step)
+                venv.step(greedy(obs))
         elif host_actions is not None:
             # the runner's numpy loop: host actions in, host arrays and the
             # lazy infos out (each call returns after its host copies)
@@ -838,7 +845,7 @@ def run_rank(args):
                                   ".step(host int32 actions) per step: obs, agent_id, node_obs, adj as host arrays "
                                   "(per-agent axes as broadcast views of one host copy per table), rewards, costs, "
                                   "dones, LazyInfos" if args.vec_env else
-                                  f"closed loop, one torch.cuda graph per step: greedy on-device policy(obs) "
+                                  f"closed loop, one torch.cuda graph per {args.policy_graph_steps} step(s): greedy on-device policy(obs) "
                                   f"({'continuous sign(goal - pos), one kernel' if args.policy_act == 'cont' else 'discrete, three kernels'}) + "
                                   "GpuGraphVecEnv(output='torch', graph='coo').step (the one-launch step, device-side hand-off "
                                   "epoch)"

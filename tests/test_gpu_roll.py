@@ -564,3 +564,46 @@ def test_roll_capture_refuses_past_one_residency_round(N, B):
     torch.cuda.synchronize()
     _same(ref, env, "chain past one residency round")
     env.close()
+
+
+def test_captured_multi_step_policy_graph():
+    """A graph holding three policy + env.step iterations (a runner capturing
+    a stretch of its rollout: three one-launch step nodes, each taking the
+    epoch the previous one advanced on the device) replayed three times
+    equals nine two-launch steps of the same closed loop, auto-resets
+    included."""
+    import os
+    N, B, S, R, EL = 24, 1024, 3, 3, 4
+    got = []
+    for two in (True, False):
+        if two:
+            os.environ["GSM_EAGER_ONE_LAUNCH"] = "0"
+        try:
+            env, _ = _env(n_agents=N, n_envs=B, episode_length=EL, seed=23)
+            env.reset(seed=23, sync_edges=False)
+            obs = env.t["node_feat"][:, :N, :6]
+            if two:
+                for _ in range(S * R):
+                    env.step(_greedy(obs), sync_edges=False)
+            else:
+                side = torch.cuda.Stream(device=DEV)
+                side.wait_stream(torch.cuda.current_stream())
+                with torch.cuda.stream(side):
+                    _greedy(obs)
+                torch.cuda.current_stream().wait_stream(side)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    for _ in range(S):
+                        env.step(_greedy(obs), sync_edges=False)
+                for _ in range(R):
+                    g.replay()
+            torch.cuda.synchronize()
+            assert not env.roll_gave_up()
+            got.append({k: v.clone() for k, v in env.t.items()})
+            env.close()
+        finally:
+            os.environ.pop("GSM_EAGER_ONE_LAUNCH", None)
+    for k in KEYS:
+        assert torch.equal(got[0][k], got[1][k]), k
+    n = int(got[0]["edge_ptr"][-1])
+    assert torch.equal(got[0]["edge_index"][:, :n], got[1]["edge_index"][:, :n])

@@ -3,7 +3,7 @@
 #
 #   bash tools/gpu.sh tests TAG [pytest -k expr]   GPU tests + smoke
 #   bash tools/gpu.sh lines TAG [line ...]         bench lines (default: all)
-#        line: h driver c2 c3 c4 n6 n12 eager policy policyg policygc buffer vecenv_c2 vecenv_h
+#        line: h driver c2 c3 c4 n6 n12 eager policy policyg policygc policyg10 policygc10 buffer vecenv_c2 vecenv_h
 #   bash tools/gpu.sh pmc TAG [which ...]          PMC passes -> profiles/pmc_kernels.json
 #        which: h c2 c3 c4 n6 n12 buffer (rollouts), h_step c4_step h_lag c4_lag
 #   bash tools/gpu.sh prof TAG [line ...]          rocprofv3 --kernel-trace --stats of bench lines
@@ -33,6 +33,8 @@ line_args() {
     policy) echo "--policy --steps 200 --warmup 20 --no-cpu-baseline" ;;
     policyg) echo "--policy-graph --steps 200 --warmup 20 --no-cpu-baseline" ;;
     policygc) echo "--policy-graph --policy-act cont --steps 200 --warmup 20 --no-cpu-baseline" ;;
+    policygc10) echo "--policy-graph --policy-graph-steps 10 --policy-act cont --steps 200 --warmup 20 --no-cpu-baseline" ;;
+    policyg10) echo "--policy-graph --policy-graph-steps 10 --steps 200 --warmup 20 --no-cpu-baseline" ;;
     buffer) echo "--buffer --no-cpu-baseline" ;;
     vecenv_c2) echo "--config c2 --vec-env numpy-dense --steps 200 --warmup 20 --no-cpu-baseline" ;;
     vecenv_h) echo "--vec-env numpy-coo --steps 100 --warmup 10 --no-cpu-baseline" ;;
@@ -92,7 +94,7 @@ case $CMD in
     timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 3; }
     tail -1 $O/smoke.log ;;
   lines)
-    for l in ${@:-h driver c2 c3 c4 n6 n12 eager policy policyg policygc buffer vecenv_c2 vecenv_h}; do run_line $l; done ;;
+    for l in ${@:-h driver c2 c3 c4 n6 n12 eager policy policyg policygc policyg10 policygc10 buffer vecenv_c2 vecenv_h}; do run_line $l; done ;;
   pmc)
     specs=""
     for w in ${@:-h c2 c3 c4 n6 n12 buffer h_lag c4_lag}; do pmc_one $w; specs="$specs $(pmc_key $w)=gpurun_out/${T}_pmc_$w"; done
