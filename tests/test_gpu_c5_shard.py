@@ -118,3 +118,53 @@ def test_c5_shards_equal_slices_of_one_batch():
         assert torch.equal(env.t["edge_index"][:, :n], buf.edge_index[T][:, :n]), r
         env.close()
     big.close()
+
+
+def test_ragged_shards_equal_slices_of_one_batch():
+    """The ragged (C4-style mixed) path sharded the same way: a scenario of
+    global id mod 3 and an N_env drawn from the global id, so two 8192-env
+    shards (env_base 0 and 8192) stepped through the fused ragged rollout
+    into rollout-buffer slots equal, step for step, their slices of one
+    16384-env batch stepped eagerly — node features, rewards, costs, done,
+    assignments, CSR edges re-based, and the final state with the
+    assignment warm-start duals — over 30 steps with an auto-reset at 20."""
+    from gsmarl_amd import EnvConfig, GpuBatchEnv, GraphRolloutBuffer
+    Nm, BA, BR, TT, EL = 24, 16384, 8192, 30, 20
+    kw = dict(scenario="mixed", n_agents=Nm, n_agents_min=3, seed=SEED, episode_length=EL)
+    gen = torch.Generator(device=DEV)
+    gen.manual_seed(SEED + 1)
+    acts = torch.randint(0, 5, (TT, BA, Nm), dtype=torch.int32, device=DEV, generator=gen)
+    shards = {}
+    for r in (0, 1):
+        env = GpuBatchEnv(EnvConfig(n_envs=BR, env_base=r * BR, **kw), DEV)
+        buf = GraphRolloutBuffer(env, episode_length=TT)
+        buf.reset(seed=SEED)
+        buf.capture(acts[:, r * BR:(r + 1) * BR].contiguous())
+        assert env.graph_is_rollout(0)
+        buf.replay()
+        buf.validate()
+        assert not bool(buf.overflowed())
+        torch.cuda.synchronize()
+        shards[r] = (env, buf)
+    big = GpuBatchEnv(EnvConfig(n_envs=BA, **kw), DEV)
+    big.reset(seed=SEED, sync_edges=False)
+    E = big.E
+    for t in range(TT):
+        big.step(acts[t], sync_edges=False)
+        ptr = big.t["edge_ptr"]
+        for r, (env, buf) in shards.items():
+            r0, r1, s = r * BR, (r + 1) * BR, t + 1
+            for k in ("node_feat", "reward", "cost", "done", "edge_count", "assign"):
+                assert torch.equal(big.t[k][r0:r1], getattr(buf, k)[s]), (r, t, k)
+            p0, p1 = int(ptr[r0]), int(ptr[r1])
+            assert torch.equal(ptr[r0:r1 + 1] - p0, buf.edge_ptr[s]), (r, t, "edge_ptr")
+            n = p1 - p0
+            assert torch.equal(big.t["edge_index"][:, p0:p1] - r0 * E, buf.edge_index[s][:, :n]), (r, t, "edges")
+            assert torch.equal(big.t["edge_attr"][p0:p1], buf.edge_attr[s][:n]), (r, t, "edge_attr")
+    torch.cuda.synchronize()
+    for r, (env, buf) in shards.items():
+        r0, r1 = r * BR, (r + 1) * BR
+        for k in STATE + ("env_shape", "lsa_v", "lsa_col"):
+            assert torch.equal(big.t[k][r0:r1], env.t[k]), (r, k)
+        env.close()
+    big.close()
