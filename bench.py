@@ -1046,6 +1046,11 @@ def kernel_roofline(env, cfg, actions, args, N, B, EL, roll=False, buf=None):
                     algorithmic_bytes_per_launch=int(k["bytes"]),
                     bytes_model=bytes_model if dom == "step" else "kernel count",
                     kernel_bytes_per_launch=int(kernel_bytes) if dom == "step" else int(k["bytes"]),
+                    # the same kernel priced at its own count of what it must
+                    # move (a fused rollout keeps the state on chip: below the
+                    # contract's §8(d) bytes), beside the contract's frac
+                    kernel_bytes_frac=round((kernel_bytes if dom == "step" else k["bytes"]) /
+                                            (k["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
                     mean_launch_us=round(k["ms"] * 1e3, 3),
                     timing=(f"HIP events around 3 back-to-back fused rollout launches of {L} steps (time per step)" if roll
                             else f"HIP events around {L} back-to-back graph launches of the kernel"),
