@@ -791,8 +791,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     const int b = blockIdx.x;
     const int tid = threadIdx.x;
     GSM_TILE_SHAPE(p);
-    float2 *s_pos = (float2 *)smem;           // [E]
-    float2 *s_vel = s_pos + E;                // [N]
+    float2 *const s_p0 = (float2 *)smem;      // [E] position buffer 0 (of three, below)
+    float2 *s_vel = s_p0 + E;                 // [N]
     float2 *s_np = s_vel + N;                 // [N] integrated agent positions
     int *s_cost = (int *)(s_np + N);          // [N]
     int *s_ired = s_cost + N;                 // [4 * kTileWaves] reduction slots
@@ -809,9 +809,17 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         q += 8 * No * W;
         sym.flag = (int *)q;
     }
-    // [2][E] positions after step k - 2 (and k), by parity: iteration k emits
-    // the edges of step k - 2
-    float2 *s_prv = (float2 *)(smem + p.wave_lds_step);
+    // Positions rotate through three LDS buffers (buffer j % 3 holds the
+    // positions before step j): step k reads buffer k % 3 and writes its
+    // agents' new positions into buffer (k + 1) % 3, and iteration k emits
+    // step k - 2's edges from buffer (k - 1) % 3 — no per-step copy of the
+    // positions and two workgroup barriers fewer per step than a single
+    // buffer plus a saved copy. Goals and obstacles (static within an
+    // episode) are kept in all three: copied at entry and, after a
+    // re-layout, into the next buffer at the end of this iteration and the
+    // one after (each after the emission that still reads the old ones)
+    float2 *s_prv = (float2 *)(smem + p.wave_lds_step);    // buffers 1 and 2
+    auto pbuf = [&](int j3) -> float2 * { return j3 == 0 ? s_p0 : s_prv + (j3 - 1) * E; };
     int *s_x = (int *)(s_prv + 2 * E);                     // [4]
     int *s_red = s_x + 4;                                  // [2 * kTileWaves] emit_env exchange
     uint32_t *s_scr = (uint32_t *)(s_red + 2 * kTileWaves);
@@ -822,7 +830,13 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     for (int w = tid; w < M * W; w += kTileBlock) s_rm[2 * M * W + w] = p.row_mask[eb * M * W + w];
     for (int w = tid; w < N * W; w += kTileBlock) s_cm[w] = p.contact_mask[eb * N * W + w];
 
-    for (int e = tid; e < E; e += kTileBlock) s_pos[e] = p.pos[eb * E + e];
+    for (int e = tid; e < E; e += kTileBlock) {
+        const float2 x = p.pos[eb * E + e];
+        s_p0[e] = x;
+        s_prv[e] = x;
+        s_prv[E + e] = x;
+    }
+    bool relaid_prev = false;   // the previous iteration re-laid the env out
     for (int i = tid; i < N; i += kTileBlock) s_vel[i] = p.vel[eb * N + i];
     int t = p.step_count[b];
     int ep = p.episode[b];
@@ -876,6 +890,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         (void)wid;
         GSM_TNOW(tp0);
         const int r3n = r3 == 2 ? 0 : r3 + 1, r3p = r3 == 0 ? 2 : r3 - 1;   // (k + 1) % 3, (k - 1) % 3
+        const float2 *const s_cur = pbuf(r3);   // positions before step k
+        float2 *const s_pos = pbuf(r3n);        // after it (agents written by the physics)
         uint64_t *const rout = s_rm + r3 * M * W;
         const uint64_t *const rkeep = s_rm + r3p * M * W;   // the previous step's masks
         const uint64_t *const remit = s_rm + r3n * M * W;   // step k - 2's masks (emitted this iteration)
@@ -918,8 +934,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
             GSM_ACC(late_params(), wid, 5, tp4);   // the prefix (last wave)
         }
         if (k >= K) __syncthreads();   // (the tail: no step; s_x[2] for the emission)
-        if (k < K) {
         bool relaid = false;
+        if (k < K) {
         auto relayout = [&]() {   // scenario.reset_world with the Philox layout
             ep = ep + 1;
             t = 0;
@@ -934,7 +950,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         // apply_environment_force + integrate_state (as gsm_step_tile_kernel)
         const uint64_t *cm = s_cm;
         for (int i = tid; i < N; i += kTileBlock) {
-            const float2 pi = s_pos[i];
+            const float2 pi = s_cur[i];
             const float2 u = roll_action_force(late_params(), arow, eb * N + i);
             float fx = 0.0f, fy = 0.0f;
             // (both read before the loop: a per-lane select of two kernarg
@@ -946,7 +962,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                     const int c = 64 * kw + __builtin_ctzll(bits);
                     bits &= bits - 1;
                     const bool ag = c < N;
-                    const float2 pj = s_pos[collider_entity(c, N)];
+                    const float2 pj = s_cur[collider_entity(c, N)];
                     const float dx = pi.x - pj.x, dy = pi.y - pj.y;
                     const float d2 = dx * dx + dy * dy;
                     const float f = contact_scale(late_params(), d2, ag ? dmin_aa : dmin_ao);
@@ -955,7 +971,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                 }
             }
             float Fx = u.x + fx, Fy = u.y + fy;
-            if (late_params().strict && strict_bad(i, pi, N, M, [&](int c) { return s_pos[collider_entity(c, N)]; })) {
+            if (late_params().strict && strict_bad(i, pi, N, M, [&](int c) { return s_cur[collider_entity(c, N)]; })) {
                 Fx = __builtin_nanf("");
                 Fy = __builtin_nanf("");
             }
@@ -972,14 +988,12 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
                 }
             }
             s_vel[i] = v;
-            s_np[i] = make_float2(pi.x + v.x * late_params().dt, pi.y + v.y * late_params().dt);
+            s_pos[i] = make_float2(pi.x + v.x * late_params().dt, pi.y + v.y * late_params().dt);
         }
         __syncthreads();
         // this workgroup's pace level (from the counter the last wave loaded
         // at the top of the iteration, published by the barrier above)
         if (k > 0 && pacing()) pace_set(__builtin_amdgcn_readfirstlane(s_x[1]));
-        for (int i = tid; i < N; i += kTileBlock) s_pos[i] = s_np[i];
-        __syncthreads();
         t += 1;
         const bool done = t >= late_params().EL;
         GSM_ACC(late_params(), wid, 0, tp0);   // physics
@@ -1088,8 +1102,8 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         GSM_ACC(late_params(), wid, 4, tp3);   // node features, publish
         }   // k < K
         // step k - 2's edges at the offset of the prefix (its positions in
-        // s_prv by parity, its masks in buffer (k - 2) % 3)
-        float2 *const s_pk = s_prv + (k & 1) * E;
+        // buffer (k - 1) % 3, its masks in buffer (k - 2) % 3)
+        const float2 *const s_pk = pbuf(r3p);
         if (k >= 2) {
             GSM_TNOW(tp5);
             int64_t off;
@@ -1105,11 +1119,19 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
         }
         if (k < K) {
             GSM_TNOW(tp6);
-            __syncthreads();   // s_pk and the staged words read
-            for (int e = tid; e < E; e += kTileBlock) s_pk[e] = s_pos[e];   // positions after step k
+            // the emission's reads of buffer (k - 1) % 3 and of the staged
+            // words done before the next step writes that buffer
+            __syncthreads();
+            // after a re-layout (this iteration or the previous one) the new
+            // goals / obstacles into the buffer the next step writes its
+            // agents into (its old ones were read by this emission)
+            if (relaid || relaid_prev) {
+                float2 *const dst = pbuf(r3n == 2 ? 0 : r3n + 1);
+                for (int e = N + tid; e < E; e += kTileBlock) dst[e] = s_pos[e];
+            }
+            relaid_prev = relaid;
             arow = arow + 1 == n_act ? 0 : arow + 1;
             if (k == K - 1) last_edges = edges;
-            __syncthreads();
             GSM_ACC(late_params(), wid, 7, tp6);   // hand-over to the next step
         }
         edges_m2 = edges_m1;
@@ -1118,7 +1140,7 @@ __global__ __launch_bounds__(kTileBlock) GSM_TILE_ATTR void gsm_roll_tile_kernel
     }
     GSM_RSTAMP(p, b * kTileWaves + (tid >> 6), 9);
     // the final state (what the next launch or an eager step reads)
-    for (int e = tid; e < E; e += kTileBlock) p.pos[eb * E + e] = s_pos[e];
+    for (int e = tid; e < E; e += kTileBlock) p.pos[eb * E + e] = pbuf(K % 3)[e];
     const int rl = (K - 1) % 3;   // the last step's masks
     for (int w = tid; w < M * W; w += kTileBlock) p.row_mask[eb * M * W + w] = s_rm[rl * M * W + w];
     for (int w = tid; w < N * W; w += kTileBlock) p.contact_mask[eb * N * W + w] = s_cm[w];
