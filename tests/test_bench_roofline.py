@@ -43,10 +43,11 @@ def test_committed_lines_fractions_at_most_one():
     shares are at most 1 and agree with counter_bound on the committed PMC."""
     import re
 
-    def order(d):   # r5_lines < r5z_lines < r6_lines
-        m = re.match(r"r(\d+)(\w*)_lines$", d.name)
+    def order(d):   # r5_lines < r5z_lines < r6_lines < r6w_package
+        m = re.match(r"r(\d+)(\w*?)_(lines|package)$", d.name)
         return (int(m.group(1)), m.group(2)) if m else (-1, "")
-    newest = max((ROOT / "profiles").glob("r*_lines"), key=order)
+    dirs = [d for d in (ROOT / "profiles").glob("r*_*") if d.is_dir() and order(d)[0] >= 0]
+    newest = max(dirs, key=order)
     lines = sorted(newest.glob("bench_*.json"))
     pmc = json.loads((ROOT / "profiles" / "pmc_kernels.json").read_text())
     assert lines and pmc["entries"]
