@@ -405,6 +405,9 @@ def parse_args(argv=None):
     # launcher self-test only (tests/test_bench_launcher.py): a CPU stand-in env
     # module and gloo; the line it prints is marked as not a measurement
     ap.add_argument("--selftest-env", default=None, help=argparse.SUPPRESS)
+    # test only (tests/test_gpu_bench_rccl.py): join a process group of one
+    # rank and run every collective of the multi-GPU path on one GPU
+    ap.add_argument("--force-pg", action="store_true", help=argparse.SUPPRESS)
     return ap.parse_args(argv)
 
 
@@ -507,8 +510,11 @@ def run_rank(args):
 
         def sync():
             torch.cuda.synchronize(dev)
-    if world > 1:
+    pg = world > 1 or args.force_pg   # the collectives of the multi-GPU path run
+    if pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if "MASTER_PORT" not in os.environ:
+            os.environ["MASTER_PORT"] = str(free_port())
         if stub:
             dist.init_process_group("gloo", rank=rank, world_size=world)
         else:   # RCCL over xGMI
@@ -696,7 +702,7 @@ def run_rank(args):
         # the region's barrier together instead of the early ones idling there
         # (and their clocks dropping, as above) for the startup skew
         sync()
-        if world > 1:
+        if pg:
             dist.barrier()
         run_steps(EL, 3)   # (the first pass runs cold: the count from the second)
         sync()
@@ -705,7 +711,7 @@ def run_rank(args):
         sync()
         settle_steps += 2 * EL
         passes = max(2, -(-int(args.settle_ms * 1e3) // max(1, int((time.perf_counter() - t_s) * 1e6))))
-        if world > 1:
+        if pg:
             pt = torch.tensor([passes], dtype=torch.int64, device=dev)
             dist.all_reduce(pt, op=dist.ReduceOp.MAX)
             passes = int(pt.item())
@@ -723,7 +729,7 @@ def run_rank(args):
         run_steps(A, a_slot)
     lsa0 = env.lsa_warm_stats() if lsa_stats else None
     sync()
-    if world > 1:
+    if pg:
         dist.barrier()
     sync()
     # (diagnostic, GSM_BENCH_CHUNK_US=1: HIP events around every chunk of the
@@ -735,7 +741,7 @@ def run_rank(args):
     if chunk_ev:
         chunk_ev[0].record()
     for ci in range(n_chunks):
-        if world > 1:
+        if pg:
             # the only collective: the episode metrics as of this chunk's start,
             # SUM-reduced over RCCL/xGMI while the chunk's kernels run (the
             # collective waits only for the snapshot copy queued before it)
@@ -751,7 +757,7 @@ def run_rank(args):
     if pending is not None:
         pending.wait()
     sync()
-    if world > 1:
+    if pg:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     if chunk_ev:
@@ -763,7 +769,7 @@ def run_rank(args):
 
     # every rank's timed region; value uses the slowest (max over ranks)
     per_rank = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
+    if pg:
         gathered = [torch.zeros_like(per_rank) for _ in range(world)]
         dist.all_gather(gathered, per_rank)
         times = [float(g.item()) for g in gathered]
@@ -773,12 +779,12 @@ def run_rank(args):
     # a bounded in-launch wait of a fused rollout that timed out leaves invalid
     # outputs: no measurement (decided on every rank together)
     bad = 1.0 if (roll and env.roll_gave_up()) else 0.0
-    if world > 1:
+    if pg:
         bad = float(all_reduce_metrics(torch.tensor([bad, 0.0, 0.0], dtype=torch.float64, device=dev))[0].item())
     if bad:
         log("ERROR: a fused rollout launch gave up waiting on a predecessor; no valid measurement")
         env.close()
-        if world > 1:
+        if pg:
             dist.destroy_process_group()
         return 3
     # final episode metrics over all ranks (the same RCCL all-reduce)
@@ -790,7 +796,7 @@ def run_rank(args):
     seg_cfg = (N + cfg.n_obstacles) <= 64 and not cfg.ragged
     # agents per step on this rank (ragged: sum of N_env), summed over ranks
     agents = int((env.t["env_shape"] & 0xFF).sum().item()) if cfg.ragged else B * N
-    if world > 1:
+    if pg:
         agents = int(all_reduce_metrics(torch.tensor([float(agents), 0.0, 0.0], dtype=torch.float64,
                                                      device=dev))[0].item())
     value = agents * K / elapsed
@@ -872,7 +878,7 @@ def run_rank(args):
             "episode_metrics": {"envs": gb, "finished_episodes": int(episodes),
                                 "mean_last_episode_reward": round(ep_rew / gb, 4),
                                 "mean_last_episode_cost": round(ep_cost / gb, 4),
-                                "reduce": "all_reduce(SUM) over ranks" if world > 1 else "single rank"},
+                                "reduce": "all_reduce(SUM) over ranks" if pg else "single rank"},
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
@@ -883,7 +889,7 @@ def run_rank(args):
                                   "scope": "rank 0, timed region; the rest are solved cold"}
         print(json.dumps(line), flush=True)
     env.close()
-    if world > 1:
+    if pg:
         dist.destroy_process_group()
     return 0
 

@@ -35,11 +35,12 @@ def test_align_puts_an_episode_boundary_in_the_timed_region():
             assert bench.boundaries_in(P, K, EL) >= 1, (W, K)
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [1, 2, 3])
 def test_gpus_n_spawns_n_ranks_and_reduces_metrics(world):
     B = 16
+    # (world 1: --force-pg joins a one-rank group, so the collectives still run)
     r = _run(["--gpus", str(world), "--config", "c2", "--n-envs", str(B), "--steps", "20", "--warmup", "5",
-              "--selftest-env", "bench_stub_env"])
+              "--selftest-env", "bench_stub_env"] + (["--force-pg"] if world == 1 else []))
     assert r.returncode == 0, r.stderr[-2000:]
     # gloo logs its connection lines on stdout; the bench prints one JSON line (rank 0 only)
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
