@@ -20,8 +20,8 @@ policy + step captured in one torch CUDA graph), `--buffer` the rollout
 buffer (every step into its own slot). Actions are pre-generated on device
 (100 x B x N int32, uniform over the 5 discrete actions) so the timed region
 has no host work; the K timed steps are replayed from HIP graphs of one
-episode (100 steps) each, with the per-episode RCCL all-reduce of episode
-metrics between chunks when N > 1.
+episode (100 steps) each; when N > 1 the ranks' shards need no exchange,
+and the RCCL all-reduce of the episode metrics runs after the timed region.
 
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W]
        torchrun --nproc-per-node N bench.py --gpus N ...
@@ -728,6 +728,26 @@ def run_rank(args):
     if A > 0:
         run_steps(A, a_slot)
     lsa0 = env.lsa_warm_stats() if lsa_stats else None
+    # No collective inside the timed region but its barriers: the envs shard
+    # with no exchange, and the episode-metric all-reduce (RCCL) runs once
+    # after it. Beside a fused rollout, which fills every SIMD, an RCCL kernel
+    # takes wave slots the rollout's grid needs and delays its workgroups:
+    # one all-reduce per 100-step chunk overlapped with the chunks cost 7.44
+    # vs 6.83 us per step at H (one rank, same box), and on several ranks the
+    # kernel holds its slots until every peer arrives.
+    bar_t = torch.zeros(1, dtype=torch.int32, device=dev)
+
+    def region_barrier():
+        """The region's closing synchronize + barrier: a one-element RCCL
+        all-reduce queued behind the rank's work, then one synchronize — it
+        completes on a rank only once every rank's contribution, queued behind
+        that rank's graphs, has arrived. dist.barrier() (an all-reduce, then a
+        device synchronize of its own) after a synchronize: 9.9-11.7 against
+        8.9-9.2 us per step on the driver's 20-step line, one rank, same box
+        (plain 8.6-8.9; profiles/r6_ab/bench_rccl/)."""
+        if pg:
+            dist.all_reduce(bar_t)
+        sync()
     sync()
     if pg:
         dist.barrier()
@@ -737,28 +757,15 @@ def run_rank(args):
     chunk_ev = ([torch.cuda.Event(enable_timing=True) for _ in range(n_chunks + 1)]
                 if os.environ.get("GSM_BENCH_CHUNK_US") and not stub else None)
     t0 = time.perf_counter()
-    pending = None
     if chunk_ev:
         chunk_ev[0].record()
     for ci in range(n_chunks):
-        if pg:
-            # the only collective: the episode metrics as of this chunk's start,
-            # SUM-reduced over RCCL/xGMI while the chunk's kernels run (the
-            # collective waits only for the snapshot copy queued before it)
-            if pending is not None:
-                pending.wait()
-            metrics.copy_(env.episode_metrics())
-            pending = all_reduce_metrics(metrics, async_op=True)
         run_steps(chunk, 0)
         if chunk_ev:
             chunk_ev[ci + 1].record()
     if rem:
         run_steps(rem, 1)
-    if pending is not None:
-        pending.wait()
-    sync()
-    if pg:
-        dist.barrier()
+    region_barrier()
     elapsed = time.perf_counter() - t0
     if chunk_ev:
         log("timed region chunks (device us): " + ", ".join(
@@ -787,7 +794,8 @@ def run_rank(args):
         if pg:
             dist.destroy_process_group()
         return 3
-    # final episode metrics over all ranks (the same RCCL all-reduce)
+    # the episode metrics over all ranks: the RCCL all-reduce (after the
+    # timed region, see there)
     metrics.copy_(env.episode_metrics())
     all_reduce_metrics(metrics)
     ep_rew, ep_cost, episodes = (float(x) for x in metrics.cpu())

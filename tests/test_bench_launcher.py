@@ -71,3 +71,16 @@ def test_gpus_n_without_gpus_fails_instead_of_falling_back():
 def test_world_size_mismatch_is_an_error():
     r = _run(["--gpus", "2", "--steps", "2", "--selftest-env", "bench_stub_env"], {"WORLD_SIZE": "1"})
     assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr and r.stdout.strip() == ""
+
+
+def test_multi_chunk_region_reduces_metrics_after_it():
+    """A 250-step region (chunks of 100, 100 and a 50-step remainder): the
+    line's metrics are the all-reduced totals after the region."""
+    B, world = 16, 2
+    r = _run(["--gpus", str(world), "--config", "c2", "--n-envs", str(B), "--steps", "250", "--warmup", "5",
+              "--selftest-env", "bench_stub_env"])
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["steps"] == 250 and d["timed_region"]["episode_boundaries"] == 3
+    em = d["episode_metrics"]
+    assert em["reduce"].startswith("all_reduce") and em["finished_episodes"] == 3 * world * B
