@@ -1,5 +1,5 @@
-"""Rollouts while another kernel holds CUs (a stand-in for the RCCL
-all-reduce that C5 overlaps with the chunk's rollout).
+"""Rollouts while another kernel holds CUs (a stand-in for any kernel on
+another stream — an RCCL collective, a user's own work — DESIGN.md §6).
 
 Spin kernels on side streams take wave slots first, so the rollout grid no
 longer fits in one residency round. The headline (segmented) rollout must
